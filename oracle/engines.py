@@ -1,0 +1,174 @@
+"""AO-route response engines (oracle).  TEST INFRASTRUCTURE ONLY.
+
+Restates what PySCF computes inside the reference's ``vresp`` closures:
+
+* ``get_jk``  -- ``mf.get_jk / get_j / get_k`` with the density-fitted ERI
+  ``(mu nu|la si) = sum_P B[P,mu,nu] B[P,la,si]`` in PySCF's convention
+  ``vk = einsum('ijkl,jk->il', eri, dm)`` (call sites XTDA.py:518-543,
+  SF_TDA.py:273-281, XSF_TDA.py:996).
+* ``nr_uks_fxc`` -- ``ni.nr_uks_fxc`` for hermi=0 densities (XTDA.py:514):
+  rho1 from ``eval_rho`` (GGA gradient terms both ways for non-hermitian dm),
+  ``wv = w * einsum('axg,axbyg->byg', rho1, fxc)``, then for GGA
+  ``wv[0]*=.5; V = ao0^T (sum_y ao_y wv_y); V += V^T``.
+* ``nr_uks_fxc_sf_tda`` -- the reference's own ALDA0 spin-flip kernel
+  (SF_TDA.py:90-160): density-only rho1, ``wv = rho1 * fxc_sf`` (weighted).
+* ``gen_response`` (XTDA.py:482-556) and ``gen_response_sf``
+  (SF_TDA.py:246-286) closures built on those.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+GRID_BLOCK = 8192
+
+
+def _k_coeffs(mf):
+    """(c_full, c_lr) such that vk = c_full*K(B) + c_lr*K(B_lr) (XTDA.py:522-539)."""
+    omega, alpha, hyb = mf.omega, mf.alpha, mf.hyb
+    if omega == 0:
+        return hyb, 0.0
+    if mf.cderi_lr is None:
+        raise ValueError("range-separated hybrid needs cderi_lr")
+    if alpha == 0:      # SR only: K_sr = K - K_lr
+        return hyb, -hyb
+    if hyb == 0:        # LR only
+        return 0.0, alpha
+    return hyb, alpha - hyb
+
+
+def get_jk(cderi, dms, with_j=True, with_k=True):
+    """J[D] = sum_P B_P <B_P, D>;  K[D] = sum_P B_P D B_P  (dms: (..., nao, nao))."""
+    dms = np.asarray(dms, dtype=np.float64)
+    shape = dms.shape
+    d = dms.reshape(-1, shape[-2], shape[-1])
+    vj = vk = None
+    if with_j:
+        gam = np.einsum('pmn,xmn->xp', cderi, d, optimize=True)
+        vj = np.einsum('xp,pmn->xmn', gam, cderi, optimize=True).reshape(shape)
+    if with_k:
+        vk = np.empty_like(d)
+        for x in range(d.shape[0]):
+            t = np.matmul(cderi, d[x])               # (naux, nao, nao): B_P D
+            vk[x] = np.einsum('pml,pln->mn', t, cderi, optimize=True)
+        vk = vk.reshape(shape)
+    return vj, vk
+
+
+def get_k_total(mf, dms):
+    """Exchange with the functional's hybrid coefficients (already scaled)."""
+    c_full, c_lr = _k_coeffs(mf)
+    vk = np.zeros_like(np.asarray(dms, dtype=np.float64))
+    if c_full != 0:
+        vk += c_full * get_jk(mf.cderi, dms, with_j=False)[1]
+    if c_lr != 0:
+        vk += c_lr * get_jk(mf.cderi_lr, dms, with_j=False)[1]
+    return vk
+
+
+def _eval_rho(ao, dm, xctype):
+    """PySCF eval_rho for a non-hermitian dm (hermi=0)."""
+    c0 = ao[0] @ dm                       # c0[g,q] = sum_p phi_p D_pq
+    rho0 = np.einsum('gq,gq->g', ao[0], c0)
+    if xctype == 'LDA':
+        return rho0[None]
+    c1 = ao[0] @ dm.T                     # c1[g,q] = sum_p phi_p D_qp
+    rho = np.empty((4, ao.shape[1]))
+    rho[0] = rho0
+    for i in range(1, 4):
+        rho[i] = np.einsum('gq,gq->g', ao[i], c0) + np.einsum('gq,gq->g', c1, ao[i])
+    return rho
+
+
+def _wv_to_vmat(ao, wv, xctype):
+    """V_mu,nu from weighted potential wv (PySCF _dot_ao_ao / hermi_sum for GGA)."""
+    if xctype == 'LDA':
+        return ao[0].T @ (wv[0][:, None] * ao[0])
+    wv = wv.copy()
+    wv[0] *= .5
+    aow = np.einsum('yg,ygq->gq', wv, ao)
+    v = ao[0].T @ aow
+    return v + v.T
+
+
+def nr_uks_fxc(mf, dms):
+    """UKS XC response V[s] for densities dms (2, nz, nao, nao), hermi=0."""
+    grids, fxc, xctype = mf.grids, mf.fxc, mf.xctype
+    dms = np.asarray(dms)
+    nz, nao = dms.shape[1], dms.shape[-1]
+    ncomp = 1 if xctype == 'LDA' else 4
+    vmat = np.zeros((2, nz, nao, nao))
+    ng = grids.ngrid
+    for g0 in range(0, ng, GRID_BLOCK):
+        g1 = min(ng, g0 + GRID_BLOCK)
+        ao = grids.ao[:ncomp, g0:g1]
+        w = grids.weights[g0:g1]
+        f = fxc[:, :ncomp, :, :ncomp, g0:g1]
+        for i in range(nz):
+            rho1 = np.asarray([_eval_rho(ao, dms[s, i], xctype) for s in range(2)])
+            wv = np.einsum('axg,axbyg->byg', rho1, f) * w
+            for s in range(2):
+                vmat[s, i] += _wv_to_vmat(ao, wv[s], xctype)
+    return vmat
+
+
+def nr_uks_fxc_sf_tda(mf, dms):
+    """ALDA0 spin-flip XC response (SF_TDA.py:90-160); dms (nz, nao, nao)."""
+    grids, vxc = mf.grids, mf.fxc_sf
+    dms = np.asarray(dms)
+    nz, nao = dms.shape[0], dms.shape[-1]
+    vmat = np.zeros((nz, nao, nao))
+    ng = grids.ngrid
+    for g0 in range(0, ng, GRID_BLOCK):
+        g1 = min(ng, g0 + GRID_BLOCK)
+        ao0 = grids.ao[0, g0:g1]
+        v = vxc[g0:g1]
+        for i in range(nz):
+            rho1 = np.einsum('gp,pq,gq->g', ao0, dms[i], ao0, optimize=True)
+            wv = rho1 * v
+            # LDA: _dot_ao_ao(ao, ao, wv); GGA: wv[0]*=.5, ao0^T(ao0 wv) + h.c. == same
+            vmat[i] += ao0.T @ (wv[:, None] * ao0)
+    return vmat
+
+
+def gen_response(mf, with_j=True):
+    """Restates XTDA.gen_response (XTDA.py:482-556) for hermi=0."""
+    def vind(dm1):
+        dm1 = np.asarray(dm1, dtype=np.float64)
+        if mf.xctype == 'HF':
+            vj, vk = get_jk(mf.cderi, dm1)
+            return vj[0] + vj[1] - vk
+        v1 = nr_uks_fxc(mf, dm1)
+        hybrid = (mf.hyb != 0) or (mf.omega != 0)
+        if not hybrid:
+            if with_j:
+                vj = get_jk(mf.cderi, dm1, with_k=False)[0]
+                v1 += vj[0] + vj[1]
+            return v1
+        vk = get_k_total(mf, dm1)
+        if with_j:
+            vj = get_jk(mf.cderi, dm1, with_k=False)[0]
+            v1 += vj[0] + vj[1] - vk
+        else:
+            v1 -= vk
+        return v1
+    return vind
+
+
+def gen_response_sf(mf, method=0):
+    """Restates SF_TDA.gen_response_sf (SF_TDA.py:246-286): no J in spin flip."""
+    def vind(dm1):
+        dm1 = np.asarray(dm1, dtype=np.float64)
+        if mf.xctype == 'HF':
+            return -get_jk(mf.cderi, dm1, with_j=False)[1]
+        if method == 0:
+            v1 = nr_uks_fxc_sf_tda(mf, dm1)
+        else:
+            v1 = np.zeros_like(dm1)
+        hybrid = (mf.hyb != 0) or (mf.omega != 0)
+        if hybrid:
+            vk = mf.hyb * get_jk(mf.cderi, dm1, with_j=False)[1]
+            if mf.omega > 1e-10:
+                vk += (mf.alpha - mf.hyb) * get_jk(mf.cderi_lr, dm1, with_j=False)[1]
+            v1 -= vk
+        return v1
+    return vind

@@ -1,0 +1,171 @@
+"""Seeded synthetic open-shell problems.
+
+PySCF (integrals, grids, libxc, SCF) is not part of this framework, so the
+operators are exercised on synthetic mean fields of the exact shapes and
+structure the reference consumes:
+
+* orthonormal MO coefficients (overlap = I), ROKS ordering core|open|virtual;
+* per-spin KS Fock matrices ``diag(eps) + 1e-3 sym(N)`` and pure-HF Fock
+  matrices ``F + 1e-2 sym(N)`` (the Delta-A inputs, XTDA.py:607-613);
+* a symmetric DF factor ``B[P,mu,nu] = sym(N) * exp(-|mu-nu|/50)`` whose
+  ``sum_P B B`` is a PSD, 8-fold symmetric ERI tensor;
+* a grid with AO values/gradients, weights and an ``fxc`` kernel symmetric
+  under (s,x) <-> (t,y); an ALDA0 ``fxc_sf`` kernel (weighted).
+
+Magnitudes are calibrated so that the response part of A is ~0.05-0.1 Ha
+against orbital gaps >= 0.25 Ha, giving a positive spectrum that the
+reference's Davidson criteria (pick w > 1e-3) handle the way they do for
+real molecules.  Seed 20261015 is the default.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .meanfield import Grid, MeanField, Mole
+
+DEFAULT_SEED = 20261015
+
+
+def _sym(rng, n, scale=1.0):
+    g = rng.standard_normal((n, n))
+    return (g + g.T) * (scale / np.sqrt(2.0))
+
+
+def _orthonormal(rng, n):
+    q, r = np.linalg.qr(rng.standard_normal((n, n)))
+    return q * np.sign(np.diag(r))
+
+
+def df_scale(nao, naux, nocc, nvir, target=0.08, decay=50.0):
+    """Entry scale for B so that the Coulomb block of A has norm ~ target."""
+    k = np.arange(nao)
+    d2 = np.exp(-2.0 * np.abs(k[:, None] - k[None, :]) / decay)
+    std_mo = np.sqrt(d2.mean())
+    sigma = np.sqrt(target) / (np.sqrt(naux) + np.sqrt(max(1, nocc * nvir)))
+    return sigma / std_mo
+
+
+def grid_scale(ngrid, nocc, nvir, target=0.05):
+    """AO-value scale so the XC block of A has norm ~ target."""
+    mean_wf = 0.275 / ngrid
+    return (target / (mean_wf * (np.sqrt(ngrid) + np.sqrt(max(1, nocc * nvir))) ** 2)) ** 0.25
+
+
+def make_df_tensor(rng, nao, naux, scale, decay=50.0):
+    k = np.arange(nao)
+    dmat = np.exp(-np.abs(k[:, None] - k[None, :]) / decay)
+    b = rng.standard_normal((naux, nao, nao))
+    b = (b + b.transpose(0, 2, 1)) * (scale / np.sqrt(2.0))
+    b *= dmat[None]
+    return b
+
+
+def make_grid(rng, nao, ngrid, ncomp, scale):
+    ao = rng.standard_normal((ncomp, ngrid, nao)) * scale
+    w = rng.uniform(0.0, 1.0, ngrid) / ngrid
+    return Grid(ao=ao, weights=w)
+
+
+def make_fxc(rng, ngrid, ncomp):
+    """UKS kernel (2,ncomp,2,ncomp,ngrid) symmetric under (s,x)<->(t,y)."""
+    n = 2 * ncomp
+    f = rng.standard_normal((n, n, ngrid)) * 0.01
+    f = 0.5 * (f + f.transpose(1, 0, 2))
+    for s in range(2):
+        for t in range(2):
+            v = -rng.uniform(0.1, 1.0, ngrid)
+            f[s * ncomp, t * ncomp] = v
+            f[t * ncomp, s * ncomp] = v
+    return f.reshape(2, ncomp, 2, ncomp, ngrid)
+
+
+def make_mf(nao=24, nc=5, no=2, naux=None, ngrid=None, xctype="GGA", hyb=0.2,
+            omega=0.0, alpha=0.0, kind="RO", seed=DEFAULT_SEED,
+            jk_target=0.08, xc_target=0.05) -> MeanField:
+    """Build a seeded synthetic ROKS ('RO') or UKS ('U') mean field.
+
+    nc / no are the closed / open shell counts (2S = no); nvir = nao-nc-no.
+    ``xctype='HF'`` gives a pure Hartree-Fock response (no grid).
+    ``omega != 0`` adds a long-range DF factor (range-separated hybrid).
+    """
+    rng = np.random.default_rng(seed)
+    nmo = nao
+    nv = nmo - nc - no
+    if nv < 1 or nc < 1:
+        raise ValueError("need at least one core and one virtual orbital")
+    naux = naux if naux is not None else 3 * nao
+    ngrid = ngrid if ngrid is not None else 60 * nao
+    ncomp = 4 if xctype == "GGA" else 1
+
+    eps_c = np.sort(rng.uniform(-1.0, -0.5, nc))
+    eps_o = np.sort(rng.uniform(-0.45, -0.25, no))
+    eps_v = np.sort(rng.uniform(0.05, 3.0, nv))
+    eps = np.concatenate([eps_c, eps_o, eps_v])
+
+    def fock_pair(shift_o_a, shift_o_b):
+        ea = eps.copy(); eb = eps.copy()
+        ea[nc:nc + no] += shift_o_a
+        eb[nc:nc + no] += shift_o_b
+        eb[:nc] += 0.02
+        eb[nc + no:] += 0.02
+        fa = np.diag(ea) + _sym(rng, nmo, 1e-3)
+        fb = np.diag(eb) + _sym(rng, nmo, 1e-3)
+        return fa, fb
+
+    fa_mo, fb_mo = fock_pair(-0.05, 0.15)
+    fa_hf = fa_mo + _sym(rng, nmo, 1e-2)
+    fb_hf = fb_mo + _sym(rng, nmo, 1e-2)
+
+    if kind == "RO":
+        c = _orthonormal(rng, nao)
+        mo_coeff = c
+        mo_occ = np.concatenate([np.full(nc, 2.0), np.full(no, 1.0), np.zeros(nv)])
+        mo_energy = eps.copy()
+        ca = cb = c
+    elif kind == "U":
+        ca = _orthonormal(rng, nao)
+        rot = _orthonormal(rng, nao)
+        # beta orbitals: a small rotation of the alpha set
+        cb = ca @ (np.eye(nao) + 0.05 * (rot - rot.T))
+        cb, r = np.linalg.qr(cb)
+        cb = cb * np.sign(np.diag(r))
+        mo_coeff = np.asarray([ca, cb])
+        occa = np.zeros(nmo); occa[:nc + no] = 1
+        occb = np.zeros(nmo); occb[:nc] = 1
+        mo_occ = np.asarray([occa, occb])
+        mo_energy = np.asarray([np.diag(fa_mo).copy(), np.diag(fb_mo).copy()])
+    else:
+        raise ValueError("kind must be 'RO' or 'U'")
+
+    h1e = _sym(rng, nao, 0.1)
+    fa_ao = ca @ fa_mo @ ca.T
+    fb_ao = cb @ fb_mo @ cb.T
+    veff = np.asarray([fa_ao - h1e, fb_ao - h1e])
+    veff_hf = np.asarray([ca @ fa_hf @ ca.T - h1e, cb @ fb_hf @ cb.T - h1e])
+
+    nocc, nvir = nc + no, no + nv
+    cderi = make_df_tensor(rng, nao, naux, df_scale(nao, naux, nocc, nvir, jk_target))
+    cderi_lr = None
+    if omega != 0.0:
+        cderi_lr = make_df_tensor(rng, nao, naux, 0.5 * df_scale(nao, naux, nocc, nvir, jk_target))
+
+    grids = fxc = fxc_sf = None
+    if xctype != "HF":
+        grids = make_grid(rng, nao, ngrid, ncomp, grid_scale(ngrid, nocc, nvir, xc_target))
+        fxc = make_fxc(rng, ngrid, ncomp)
+        fxc_sf = -rng.uniform(0.1, 1.0, ngrid) * grids.weights
+    else:
+        hyb, alpha, omega = 1.0, 0.0, 0.0
+
+    mol = Mole(nao=nao, spin=no, nelectron=2 * nc + no)
+    return MeanField(mol=mol, mo_coeff=mo_coeff, mo_occ=mo_occ, mo_energy=mo_energy,
+                     h1e=h1e, veff=veff, veff_hf=veff_hf, cderi=cderi, grids=grids,
+                     fxc=fxc, fxc_sf=fxc_sf, cderi_lr=cderi_lr, xctype=xctype,
+                     omega=omega, alpha=alpha, hyb=hyb)
+
+
+def make_trial_vectors(nz, dim, seed=DEFAULT_SEED + 1):
+    """Row-normalised N(0,1) trial vectors."""
+    rng = np.random.default_rng(seed)
+    z = rng.standard_normal((nz, dim))
+    return z / np.linalg.norm(z, axis=1, keepdims=True)
