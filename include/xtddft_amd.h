@@ -1,0 +1,122 @@
+/* xtddft_amd -- MI355X-native TDA response hot path (C ABI).
+ *
+ * Drop-in boundary for the Davidson/TDA operator of
+ * Quantum-Chemistry-Group-BNU/XTDDFT.  Each entry point names the reference
+ * interface it replaces (file:line relative to the reference root).  All
+ * arrays are FP64, row-major, caller-owned; setters copy into device memory
+ * owned by the context.  `ptr_kind` is XT_PTR_HOST or XT_PTR_DEVICE.
+ * Every call returns 0 on success or a negative XT_ERR_* code; the message of
+ * the last failure is available from xt_last_error().
+ */
+#ifndef XTDDFT_AMD_H
+#define XTDDFT_AMD_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XT_ABI_VERSION 1
+
+#define XT_PTR_HOST 0
+#define XT_PTR_DEVICE 1
+
+/* operator kinds */
+#define XT_KIND_XTDA 0     /* spin-adapted X-TDA on ROKS        (XTDA.py:558-692, self.X)   */
+#define XT_KIND_UTDA 1     /* unrestricted TDA on UKS          (XTDA.py:685-687)            */
+#define XT_KIND_SF_DOWN 2  /* spin-flip down  (SF_TDA.py:162-244, isf=-1)                   */
+#define XT_KIND_SF_UP 3    /* spin-flip up    (SF_TDA.py:162-244, isf=+1)                   */
+#define XT_KIND_XSF 4      /* spin-adapted spin-flip down (XSF_TDA.py:1029-1277)           */
+
+/* exchange-correlation kernel types */
+#define XT_XC_NONE 0       /* pure Hartree-Fock response (XTDA.py:546-554)                 */
+#define XT_XC_LDA 1
+#define XT_XC_GGA 2
+
+typedef struct xt_ctx xt_ctx;
+
+typedef struct xt_desc {
+  int kind;          /* XT_KIND_* */
+  int restricted;    /* 1: ROKS (one MO basis), 0: UKS (alpha/beta bases) */
+  int nao, nmo;
+  int nc, no, nv;    /* closed / open / virtual counts (utils.get_cov, utils.py:6-41) */
+  int naux;          /* DF functions held by THIS context (a shard when distributed) */
+  int ngrid;         /* grid points held by THIS context */
+  int xctype;        /* XT_XC_* */
+  double hyb;        /* rsh_and_hybrid_coeff (XTDA.py:501) */
+  double alpha;
+  double omega;      /* != 0: long-range factor set with xt_set_jk_df(which=1) */
+  double si;         /* spin/2 (XTDA.py:613); XSF uses no/2 (XSF_TDA.py:1061) */
+  int sa;            /* XSF spin-adaptation level 0..3 (XSF_TDA.py:148-152) */
+  double foo, fglobal; /* XSF scale factors (XSF_TDA.py:1501-1518) */
+  int remove;        /* XSF: compress the OO block by one vector (XSF_TDA.py:397-414) */
+  int add_local;     /* 1: add the rank-local one-electron terms (Fock, Delta-A Fock
+                        parts); set on exactly one rank of a sharded operator */
+  int device;        /* HIP device ordinal */
+} xt_desc;
+
+/* lifetime ------------------------------------------------------------- */
+int xt_create(const xt_desc* desc, xt_ctx** out);
+int xt_destroy(xt_ctx* ctx);
+int xt_set_stream(xt_ctx* ctx, void* hip_stream);
+const char* xt_last_error(void);
+int xt_abi_version(void);
+
+/* one-time setup (what the reference builds once per solve) ------------ */
+/* MO coefficients (nao x nmo); c_beta ignored when restricted.
+   Replaces mf.mo_coeff consumption in _gen_tda_operation (XTDA.py:565-586). */
+int xt_set_orbitals(xt_ctx* ctx, const double* c_alpha, const double* c_beta, int ptr_kind);
+/* KS and pure-HF Fock matrices in the MO basis (nmo x nmo each), or the orbital
+   energies for UTDA via xt_set_orbital_energies.
+   Replaces mf.get_veff/get_hcore + scf.ROHF(mol).get_veff (XTDA.py:588-613,
+   XSF_TDA.py:1070-1114). */
+int xt_set_fock_mo(xt_ctx* ctx, const double* fa, const double* fb,
+                   const double* fa_hf, const double* fb_hf, int ptr_kind);
+int xt_set_orbital_energies(xt_ctx* ctx, const double* e_a, const double* e_b, int ptr_kind);
+/* Density-fitting factor B[P,mu,nu] (naux x nao x nao) defining
+   (mu nu|la si) = sum_P B B.  which = 0: full-range Coulomb, 1: long-range.
+   Replaces mf.get_jk / get_j / get_k (XTDA.py:518-543, SF_TDA.py:273-281,
+   XSF_TDA.py:996) -- the AO->MO transform is done once here on the device. */
+int xt_set_jk_df(xt_ctx* ctx, const double* cderi, int which, int ptr_kind);
+/* AO values on the grid (ncomp x ngrid x nao; ncomp = 1 LDA / 4 GGA),
+   weights (ngrid) and the kernel: UKS fxc (2 x ncomp x 2 x ncomp x ngrid,
+   un-weighted) for XTDA/UTDA, or the weighted ALDA0 kernel (ngrid) for SF/XSF.
+   Replaces ni.cache_xc_kernel / cache_xc_kernel_sf (XTDA.py:504, SF_TDA.py:39-88)
+   and the per-call grid loop of ni.nr_uks_fxc / nr_uks_fxc_sf_tda
+   (XTDA.py:514, SF_TDA.py:90-160). */
+int xt_set_grid(xt_ctx* ctx, const double* ao, const double* weights,
+                const double* kernel, int ptr_kind);
+/* XSF only: OO compression basis vects (no^2 x (no^2-1)) (XSF_TDA.py:397-414). */
+int xt_set_oo_basis(xt_ctx* ctx, const double* vects, int ptr_kind);
+
+/* the hot path --------------------------------------------------------- */
+/* sigma = A z for nz trial vectors, row-major (nz x dim) in the reference's
+   vector order (PySCF order for XTDA/UTDA/SF; cv|co|ov|oo for XSF, OO
+   compressed when remove).  Replaces the vind closures (XTDA.py:615-690,
+   SF_TDA.py:224-243, XSF_TDA.py:1131-1276). */
+int xt_apply(xt_ctx* ctx, int nz, const double* z, double* sigma, int ptr_kind);
+int xt_dim(const xt_ctx* ctx);
+/* per-phase device timings of the last xt_apply (ms): jk, xc, local, total */
+int xt_last_timings(const xt_ctx* ctx, double* out4);
+
+/* XSF preconditioner J diagonals (XSF_TDA.py:859-913): co_j (nc x no), ov_j (no x nv). */
+int xt_xsf_j_diagonals(xt_ctx* ctx, double* co_j, double* ov_j, int ptr_kind);
+
+/* device linear algebra used by the Davidson solver (Davidson.py:21-298) ---- */
+/* C = alpha * op(A) op(B) + beta * C on device pointers (strided, batched);
+   trans flags: 0 = as stored row-major, 1 = transposed. */
+int xt_dgemm(int transa, int transb, int m, int n, int k, double alpha,
+             const double* a, long lda, const double* b, long ldb, double beta,
+             double* c, long ldc, void* hip_stream);
+/* y = (x - e*w) / clamp(d - (e - shift)) row-wise; diag preconditioner
+   (XTDA.py:736-744, PySCF make_diag_precond). nrow vectors of length dim. */
+int xt_precond(int nrow, int dim, const double* diag, const double* e, double shift,
+               const double* r, double* out, void* hip_stream);
+/* out[i] = sum_j x[i,j]^2 for nrow rows. */
+int xt_row_norms2(int nrow, int dim, const double* x, double* out, void* hip_stream);
+/* x[i,:] *= s[i] */
+int xt_row_scale(int nrow, int dim, double* x, const double* s, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,43 @@
+// Internal declarations shared by the HIP translation units of libxtddft_amd.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+#define XT_OK 0
+#define XT_ERR_ARG -1
+#define XT_ERR_OOM -2
+#define XT_ERR_HIP -3
+#define XT_ERR_STATE -4
+#define XT_ERR_RCCL -5
+
+namespace xt {
+
+// Public-facing GEMM description (see xt_gemm.hip for the contraction).
+struct GemmDesc {
+  int M = 0, N = 0, K = 0, R = 1;
+  int nb1 = 1, nb2 = 1;               // batch = nb1 x nb2
+  const double* A = nullptr;
+  long sAm = 0, sAk = 0, sAr = 0, sAb1 = 0, sAb2 = 0;
+  const double* B = nullptr;
+  long sBk = 0, sBn = 0, sBr = 0, sBb1 = 0, sBb2 = 0;
+  double* C = nullptr;
+  long ldc = 0, sCb1 = 0, sCb2 = 0;
+  double alpha = 1.0, beta = 0.0;
+  int max_split = 0;                  // 0 = heuristic
+};
+
+struct GemmParams {
+  int M, N, K, R;
+  int nbatch, nb2, nsplit;
+  const double* A; long sAm, sAk, sAr, sAb1, sAb2;
+  const double* B; long sBk, sBn, sBr, sBb1, sBb2;
+  double* C; long ldc, sCb1, sCb2;
+  double alpha, beta;
+  double* ws;
+};
+
+void plan_gemm(const GemmDesc& d, GemmParams* p, int* bm, int* bn);
+size_t dgemm_workspace_bytes(const GemmDesc& d);
+int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes);
+
+}  // namespace xt

@@ -1,0 +1,25 @@
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace xt {
+void embed_xtda(hipStream_t st, int nz, int nc, int no, int nv, const double* z, double* ze);
+void extract_xtda(hipStream_t st, int nz, int nc, int no, int nv, const double* acc, const double* kx, double* out);
+void extract_one(hipStream_t st, int nz, int O, int V, const double* acc, const double* kx, double* out);
+void permute_xi(hipStream_t st, int nz, int O, int V, const double* src, double* dst);
+void permute_add(hipStream_t st, int nz, int O, int V, double alpha, const double* src, double* dst);
+void permute_add_strided(hipStream_t st, int nz, int nry, int ncy, double alpha, const double* src,
+                         double* dst, long ldS, long svS);
+void xsf_rank1(hipStream_t st, int nz, int nc, int no, int nv, int nmo, double a2, double a4,
+               const double* ze, const double* fs, const double* fa, const double* fb, double* acc);
+void ediag(hipStream_t st, int nz, int O, int V, int nmo, int v0, const double* eps, const double* ze, double* acc);
+void xc_uks(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, int nmo,
+            const double* phi0, const double* phi1, const double* wfxc, double* U);
+void xc_sf(hipStream_t st, int G, int g0, int nz, int O, int nmo, const double* phio, const double* fsf, double* U);
+void weight_fxc(hipStream_t st, long n4, int ngrid, const double* w, double* f);
+void xsf_assemble(hipStream_t st, int nz, int nc, int no, int nv, int remove, const double* vects, const double* z, double* ze);
+void xsf_extract(hipStream_t st, int nz, int nc, int no, int nv, int remove, const double* vects, const double* full, double* out);
+void xsf_jdiag(hipStream_t st, int naux, int nmo, int nc, int no, int nv, const double* bmo, double* co_j, double* ov_j);
+void precond(hipStream_t st, int nrow, int dim, const double* diag, const double* e, double shift, const double* r, double* out);
+void row_norms2(hipStream_t st, int nrow, int dim, const double* x, double* out);
+void row_scale(hipStream_t st, int nrow, int dim, double* x, const double* s);
+}  // namespace xt

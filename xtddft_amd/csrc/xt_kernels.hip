@@ -1,0 +1,473 @@
+// Element-wise / gather kernels of the TDA hot path (gfx950).
+//
+// Layout conventions (all FP64, row-major):
+//   Ze   (nz, O, V)    one spin channel's trial vectors embedded in the
+//                      superset occupied (O = nc+no) x virtual (V = no+nv)
+//                      block; positions outside the channel's own block are 0.
+//   Phi  (ncomp, ngrid, nmo) MO values/gradients on the grid.
+//   U/S  (ncomp, G, nz*O)    per grid chunk: U_c = PhiV^c Ze^T, overwritten
+//                            in place by the back-projection factors S_c.
+#include <hip/hip_runtime.h>
+#include "xt_internal.h"
+#include "xt_kernels.h"
+
+namespace xt {
+
+static inline int nblocks(long n, int bs = 256, int cap = 65536) {
+  long b = (n + bs - 1) / bs;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+#define GRID_STRIDE(i, n) \
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (n); i += (long)gridDim.x * blockDim.x)
+
+// ---- X-TDA / U-TDA: PySCF-order vectors <-> embedded channels -------------
+// za (nocc_a = O, nvir_a = nv) sits at columns [no, V); zb (nocc_b = nc, nvir_b = V)
+// sits at rows [0, nc)  (XTDA.py:619-620).
+__global__ void k_embed_xtda(int nz, int nc, int no, int nv, const double* __restrict__ z,
+                             double* __restrict__ ze) {
+  const int O = nc + no, V = no + nv;
+  const long dim = (long)O * nv + (long)nc * V;
+  const long n = 2L * nz * O * V;
+  GRID_STRIDE(t, n) {
+    long r = t;
+    const int a = (int)(r % V); r /= V;
+    const int i = (int)(r % O); r /= O;
+    const int x = (int)(r % nz);
+    const int ch = (int)(r / nz);
+    double v = 0.0;
+    if (ch == 0) {
+      if (a >= no) v = z[x * dim + (long)i * nv + (a - no)];
+    } else {
+      if (i < nc) v = z[x * dim + (long)O * nv + (long)i * V + a];
+    }
+    ze[t] = v;
+  }
+}
+
+// sigma_out = acc - kx (kx in (O, nz, V) layout per channel)
+__global__ void k_extract_xtda(int nz, int nc, int no, int nv, const double* __restrict__ acc,
+                               const double* __restrict__ kx, double* __restrict__ out) {
+  const int O = nc + no, V = no + nv;
+  const long dim = (long)O * nv + (long)nc * V;
+  const long chs = (long)nz * O * V;
+  GRID_STRIDE(t, (long)nz * dim) {
+    const int x = (int)(t / dim);
+    const long e = t % dim;
+    int ch, i, a;
+    if (e < (long)O * nv) { ch = 0; i = (int)(e / nv); a = (int)(e % nv) + no; }
+    else { const long f = e - (long)O * nv; ch = 1; i = (int)(f / V); a = (int)(f % V); }
+    double v = acc[ch * chs + ((long)x * O + i) * V + a];
+    if (kx) v -= kx[ch * chs + ((long)i * nz + x) * V + a];
+    out[t] = v;
+  }
+}
+
+// Single channel (SF / XSF): sigma = acc - kx
+__global__ void k_extract_one(int nz, int O, int V, const double* __restrict__ acc,
+                              const double* __restrict__ kx, double* __restrict__ out) {
+  GRID_STRIDE(t, (long)nz * O * V) {
+    const int a = (int)(t % V);
+    const long r = t / V;
+    const int i = (int)(r % O);
+    const int x = (int)(r / O);
+    double v = acc[t];
+    if (kx) v -= kx[((long)i * nz + x) * V + a];
+    out[t] = v;
+  }
+}
+
+// (nz, O, V) -> (O, nz, V)
+__global__ void k_permute_xi(int nz, int O, int V, const double* __restrict__ src,
+                             double* __restrict__ dst) {
+  GRID_STRIDE(t, (long)nz * O * V) {
+    const int a = (int)(t % V);
+    const long r = t / V;
+    const int x = (int)(r % nz);
+    const int i = (int)(r / nz);
+    dst[t] = src[((long)x * O + i) * V + a];
+  }
+}
+
+// dst(nz, O, V) += alpha * src(O, nz, V)
+__global__ void k_permute_add(int nz, int O, int V, double alpha, const double* __restrict__ src,
+                              double* __restrict__ dst) {
+  GRID_STRIDE(t, (long)nz * O * V) {
+    const int a = (int)(t % V);
+    const long r = t / V;
+    const int i = (int)(r % O);
+    const int x = (int)(r / O);
+    dst[t] += alpha * src[((long)i * nz + x) * V + a];
+  }
+}
+
+// S[x*svS + j*ldS + b] += alpha * src[(j*nz + x)*ncy + b]
+__global__ void k_permute_add_strided(int nz, int nry, int ncy, double alpha, const double* __restrict__ src,
+                                      double* __restrict__ dst, long ldS, long svS) {
+  GRID_STRIDE(t, (long)nz * nry * ncy) {
+    const int b = (int)(t % ncy);
+    const long r = t / ncy;
+    const int x = (int)(r % nz);
+    const int j = (int)(r / nz);
+    dst[(long)x * svS + (long)j * ldS + b] += alpha * src[t];
+  }
+}
+
+// XSF trace / rank-one Delta-A terms, one block per trial vector (XSF_TDA.py:1235-1269):
+//   t_oo = tr(oo), t_cv = <fs_cv, cv>, t_co = <fB_co, co>, t_ov = sum fA_vo[a,u] ov[u,a]
+//   cv += a2*fs_cv*t_oo ; co += a4*fB_co*t_oo ; ov -= a4*fA_vo^T*t_oo
+//   oo_vv += a2*t_cv + a4*(t_co - t_ov)          (a2 = fg*foo*f2/si, a4 = fg*foo*f4)
+__global__ void k_xsf_rank1(int nz, int nc, int no, int nv, int nmo, double a2, double a4,
+                            const double* __restrict__ ze, const double* __restrict__ fs,
+                            const double* __restrict__ fa, const double* __restrict__ fb,
+                            double* __restrict__ acc) {
+  __shared__ double red[4][256];
+  const int x = blockIdx.x;
+  const int O = nc + no, V = no + nv;
+  const int mo = nc, mv = nc + no;
+  const double* z = ze + (long)x * O * V;
+  double* s = acc + (long)x * O * V;
+  double t[4] = {0, 0, 0, 0};
+  for (int k = threadIdx.x; k < no; k += blockDim.x) t[0] += z[(long)(nc + k) * V + k];
+  for (long k = threadIdx.x; k < (long)nc * nv; k += blockDim.x) {
+    const int i = (int)(k / nv), a = (int)(k % nv);
+    t[1] += fs[(long)i * nmo + mv + a] * z[(long)i * V + no + a];
+  }
+  for (long k = threadIdx.x; k < (long)nc * no; k += blockDim.x) {
+    const int i = (int)(k / no), u = (int)(k % no);
+    t[2] += fb[(long)i * nmo + mo + u] * z[(long)i * V + u];
+  }
+  for (long k = threadIdx.x; k < (long)no * nv; k += blockDim.x) {
+    const int u = (int)(k / nv), a = (int)(k % nv);
+    t[3] += fa[(long)(mv + a) * nmo + mo + u] * z[(long)(nc + u) * V + no + a];
+  }
+  for (int q = 0; q < 4; ++q) red[q][threadIdx.x] = t[q];
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) for (int q = 0; q < 4; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + w];
+    __syncthreads();
+  }
+  const double t_oo = red[0][0], t_cv = red[1][0], t_co = red[2][0], t_ov = red[3][0];
+  for (long k = threadIdx.x; k < (long)nc * nv; k += blockDim.x) {
+    const int i = (int)(k / nv), a = (int)(k % nv);
+    s[(long)i * V + no + a] += a2 * fs[(long)i * nmo + mv + a] * t_oo;
+  }
+  for (long k = threadIdx.x; k < (long)nc * no; k += blockDim.x) {
+    const int i = (int)(k / no), u = (int)(k % no);
+    s[(long)i * V + u] += a4 * fb[(long)i * nmo + mo + u] * t_oo;
+  }
+  for (long k = threadIdx.x; k < (long)no * nv; k += blockDim.x) {
+    const int u = (int)(k / nv), a = (int)(k % nv);
+    s[(long)(nc + u) * V + no + a] -= a4 * fa[(long)(mv + a) * nmo + mo + u] * t_oo;
+  }
+  for (int v = threadIdx.x; v < no; v += blockDim.x)
+    s[(long)(nc + v) * V + v] += a2 * t_cv + a4 * (t_co - t_ov);
+}
+
+// U-TDA orbital-energy term: acc[ch][x][i][a] += (eps_v[a] - eps_o[i]) * ze[ch][x][i][a]
+// (XTDA.py:685-687).  eps_* of channel ch live at eps + ch*nmo.
+__global__ void k_ediag(int nz, int O, int V, int nmo, int v0, const double* __restrict__ eps,
+                        const double* __restrict__ ze, double* __restrict__ acc) {
+  const long chs = (long)nz * O * V;
+  GRID_STRIDE(t, 2 * chs) {
+    const int ch = (int)(t / chs);
+    const long e = t % chs;
+    const int a = (int)(e % V);
+    const int i = (int)((e / V) % O);
+    const double* ep = eps + (long)ch * nmo;
+    acc[t] += (ep[v0 + a] - ep[i]) * ze[t];
+  }
+}
+
+// ---- XC response on the grid, UKS kernel (PySCF nr_uks_fxc semantics) ----
+// For each grid point g and vector x (one 64-lane wave):
+//   rho1[s][0]  = sum_i U0[s][g][x,i] * PhiO0[s][g][i]
+//   rho1[s][c]  = sum_i (U0 PhiOc + Uc PhiO0)        c = 1..3 (GGA)
+//   wv[s][y]    = sum_{t,y'} wfxc[t,y'][s,y][g] rho1[t][y']   (weight folded in)
+//   S0[s][g][x,i] = wv0 PhiO0 + sum_c wvc PhiOc ;  Sc = wvc PhiO0
+// U is overwritten by S.  U layout: (nch, ncomp, G, nz*O); PhiO of channel s
+// is phi[s] + comp*ngrid*nmo + (g0+g)*nmo + i.
+template <int NC>
+__global__ void __launch_bounds__(256)
+k_xc_uks(int G, int g0, int ngrid, int nz, int O, int nmo,
+         const double* __restrict__ phi0, const double* __restrict__ phi1,
+         const double* __restrict__ wfxc, double* __restrict__ U) {
+  const int lane = threadIdx.x & 63;
+  const long wid = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 6;
+  const long nwork = (long)G * nz;
+  if (wid >= nwork) return;
+  const int g = (int)(wid / nz);
+  const int x = (int)(wid % nz);
+  const long ldU = (long)nz * O;
+  const long compU = (long)G * ldU;
+  const long chU = NC * compU;
+  const long compP = (long)ngrid * nmo;
+  const double* phis[2] = {phi0, phi1};
+
+  double rho[2][NC];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const double* ph = phis[s] + (long)(g0 + g) * nmo;
+    const double* u = U + s * chU + (long)g * ldU + (long)x * O;
+    double acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = 0.0;
+    for (int i = lane; i < O; i += 64) {
+      const double u0 = u[i];
+      const double p0 = ph[i];
+      acc[0] += u0 * p0;
+#pragma unroll
+      for (int c = 1; c < NC; ++c)
+        acc[c] += u0 * ph[c * compP + i] + u[c * compU + i] * p0;
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      double v = acc[c];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      rho[s][c] = v;
+    }
+  }
+  // wv[s][y] = sum_{t,y'} f[t,y',s,y] rho[t][y']  ; f layout (2,NC,2,NC,ngrid)
+  double wv[2][NC];
+  const long gg = g0 + g;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int y = 0; y < NC; ++y) {
+      double v = 0.0;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int yy = 0; yy < NC; ++yy)
+          v += wfxc[((((long)t * NC + yy) * 2 + s) * NC + y) * ngrid + gg] * rho[t][yy];
+      wv[s][y] = v;
+    }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const double* ph = phis[s] + (long)(g0 + g) * nmo;
+    double* u = U + s * chU + (long)g * ldU + (long)x * O;
+    for (int i = lane; i < O; i += 64) {
+      const double p0 = ph[i];
+      double s0 = wv[s][0] * p0;
+#pragma unroll
+      for (int c = 1; c < NC; ++c) {
+        s0 += wv[s][c] * ph[c * compP + i];
+        u[c * compU + i] = wv[s][c] * p0;
+      }
+      u[i] = s0;
+    }
+  }
+}
+
+// ALDA0 spin-flip kernel (SF_TDA.py:90-160): rho1 = sum_i U0 PhiO, wv = rho1*fsf, S0 = wv*PhiO
+__global__ void __launch_bounds__(256)
+k_xc_sf(int G, int g0, int nz, int O, int nmo, const double* __restrict__ phio,
+        const double* __restrict__ fsf, double* __restrict__ U) {
+  const int lane = threadIdx.x & 63;
+  const long wid = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 6;
+  if (wid >= (long)G * nz) return;
+  const int g = (int)(wid / nz);
+  const int x = (int)(wid % nz);
+  const double* ph = phio + (long)(g0 + g) * nmo;
+  double* u = U + (long)g * nz * O + (long)x * O;
+  double acc = 0.0;
+  for (int i = lane; i < O; i += 64) acc += u[i] * ph[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  const double wv = acc * fsf[g0 + g];
+  for (int i = lane; i < O; i += 64) u[i] = wv * ph[i];
+}
+
+// wfxc = fxc * w  (fxc layout (2,nc,2,nc,ngrid))
+__global__ void k_weight_fxc(long n4, int ngrid, const double* __restrict__ w, double* __restrict__ f) {
+  GRID_STRIDE(t, n4 * ngrid) f[t] *= w[t % ngrid];
+}
+
+// ---- XSF: cv|co|ov|oo blocks <-> full (nocc_a x nvir_b) spin-flip block ----
+// full Z[i][a'] rows i: c then o; cols a': o then v.  OO optionally expanded
+// by the compression basis vects (no^2 x (no^2-1)) (XSF_TDA.py:1011-1027).
+__global__ void k_xsf_assemble(int nz, int nc, int no, int nv, int remove,
+                               const double* __restrict__ vects, const double* __restrict__ z,
+                               double* __restrict__ ze) {
+  const int O = nc + no, V = no + nv;
+  const long d1 = (long)nc * nv, d2 = d1 + (long)nc * no, d3 = d2 + (long)no * nv;
+  const long dim = d3 + (long)no * no - (remove ? 1 : 0);
+  GRID_STRIDE(t, (long)nz * O * V) {
+    const int a = (int)(t % V);
+    const long r = t / V;
+    const int i = (int)(r % O);
+    const int x = (int)(r / O);
+    const double* zx = z + x * dim;
+    double v;
+    if (i < nc) {
+      v = (a >= no) ? zx[(long)i * nv + (a - no)] : zx[d1 + (long)i * no + a];
+    } else {
+      const int u = i - nc;
+      if (a >= no) v = zx[d2 + (long)u * nv + (a - no)];
+      else {
+        const int row = u * no + a;
+        if (remove) {
+          const int m = no * no - 1;
+          double s = 0.0;
+          for (int y = 0; y < m; ++y) s += vects[(long)row * m + y] * zx[d3 + y];
+          v = s;
+        } else {
+          v = zx[d3 + row];
+        }
+      }
+    }
+    ze[t] = v;
+  }
+}
+
+// full (nz, O, V) sigma -> cv|co|ov|oo (OO compressed with vects^T when remove)
+__global__ void k_xsf_extract(int nz, int nc, int no, int nv, int remove,
+                              const double* __restrict__ vects, const double* __restrict__ full,
+                              double* __restrict__ out) {
+  const int O = nc + no, V = no + nv;
+  const long d1 = (long)nc * nv, d2 = d1 + (long)nc * no, d3 = d2 + (long)no * nv;
+  const int noo = no * no - (remove ? 1 : 0);
+  const long dim = d3 + noo;
+  GRID_STRIDE(t, (long)nz * dim) {
+    const int x = (int)(t / dim);
+    const long e = t % dim;
+    const double* f = full + (long)x * O * V;
+    double v;
+    if (e < d1) { const int i = (int)(e / nv), a = (int)(e % nv); v = f[(long)i * V + no + a]; }
+    else if (e < d2) { const long k = e - d1; const int i = (int)(k / no), u = (int)(k % no); v = f[(long)i * V + u]; }
+    else if (e < d3) { const long k = e - d2; const int u = (int)(k / nv), a = (int)(k % nv); v = f[(long)(nc + u) * V + no + a]; }
+    else {
+      const int y = (int)(e - d3);
+      if (remove) {
+        const int m = no * no - 1;
+        double s = 0.0;
+        for (int row = 0; row < no * no; ++row)
+          s += vects[(long)row * m + y] * f[(long)(nc + row / no) * V + (row % no)];
+        v = s;
+      } else {
+        v = f[(long)(nc + y / no) * V + (y % no)];
+      }
+    }
+    out[t] = v;
+  }
+}
+
+// XSF J diagonals: co_j[i][u] = sum_P B[P][i][nc+u]^2 ; ov_j[u][a] = sum_P B[P][nc+u][nc+no+a]^2
+__global__ void k_xsf_jdiag(int naux, int nmo, int nc, int no, int nv, const double* __restrict__ bmo,
+                            double* __restrict__ co_j, double* __restrict__ ov_j) {
+  const long nco = (long)nc * no, nov = (long)no * nv;
+  GRID_STRIDE(t, nco + nov) {
+    long row, col;
+    if (t < nco) { row = t / no; col = nc + t % no; }
+    else { const long k = t - nco; row = nc + k / nv; col = nc + no + k % nv; }
+    double s = 0.0;
+    for (int P = 0; P < naux; ++P) {
+      const double b = bmo[(long)P * nmo * nmo + row * nmo + col];
+      s += b * b;
+    }
+    if (t < nco) co_j[t] = s; else ov_j[t - nco] = s;
+  }
+}
+
+// ---- Davidson helpers -----------------------------------------------------
+__global__ void k_precond(int nrow, int dim, const double* __restrict__ diag, const double* __restrict__ e,
+                          double shift, const double* __restrict__ r, double* __restrict__ out) {
+  GRID_STRIDE(t, (long)nrow * dim) {
+    const int row = (int)(t / dim);
+    double d = diag[t % dim] - (e[row] - shift);
+    if (fabs(d) < 1e-8) d = 1e-8;
+    out[t] = r[t] / d;
+  }
+}
+
+__global__ void k_row_norms2(int nrow, int dim, const double* __restrict__ x, double* __restrict__ out) {
+  __shared__ double red[256];
+  const int row = blockIdx.x;
+  double s = 0.0;
+  for (long j = threadIdx.x; j < dim; j += blockDim.x) { const double v = x[(long)row * dim + j]; s += v * v; }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[row] = red[0];
+}
+
+__global__ void k_row_scale(int nrow, int dim, double* __restrict__ x, const double* __restrict__ s) {
+  GRID_STRIDE(t, (long)nrow * dim) x[t] *= s[t / dim];
+}
+
+// ---- launch wrappers --------------------------------------------------------
+void embed_xtda(hipStream_t st, int nz, int nc, int no, int nv, const double* z, double* ze) {
+  const long n = 2L * nz * (nc + no) * (no + nv);
+  hipLaunchKernelGGL(k_embed_xtda, dim3(nblocks(n)), dim3(256), 0, st, nz, nc, no, nv, z, ze);
+}
+void extract_xtda(hipStream_t st, int nz, int nc, int no, int nv, const double* acc, const double* kx, double* out) {
+  const long n = (long)nz * ((long)(nc + no) * nv + (long)nc * (no + nv));
+  hipLaunchKernelGGL(k_extract_xtda, dim3(nblocks(n)), dim3(256), 0, st, nz, nc, no, nv, acc, kx, out);
+}
+void extract_one(hipStream_t st, int nz, int O, int V, const double* acc, const double* kx, double* out) {
+  hipLaunchKernelGGL(k_extract_one, dim3(nblocks((long)nz * O * V)), dim3(256), 0, st, nz, O, V, acc, kx, out);
+}
+void permute_xi(hipStream_t st, int nz, int O, int V, const double* src, double* dst) {
+  hipLaunchKernelGGL(k_permute_xi, dim3(nblocks((long)nz * O * V)), dim3(256), 0, st, nz, O, V, src, dst);
+}
+void permute_add(hipStream_t st, int nz, int O, int V, double alpha, const double* src, double* dst) {
+  hipLaunchKernelGGL(k_permute_add, dim3(nblocks((long)nz * O * V)), dim3(256), 0, st, nz, O, V, alpha, src, dst);
+}
+void permute_add_strided(hipStream_t st, int nz, int nry, int ncy, double alpha, const double* src,
+                         double* dst, long ldS, long svS) {
+  hipLaunchKernelGGL(k_permute_add_strided, dim3(nblocks((long)nz * nry * ncy)), dim3(256), 0, st,
+                     nz, nry, ncy, alpha, src, dst, ldS, svS);
+}
+void xsf_rank1(hipStream_t st, int nz, int nc, int no, int nv, int nmo, double a2, double a4,
+               const double* ze, const double* fs, const double* fa, const double* fb, double* acc) {
+  hipLaunchKernelGGL(k_xsf_rank1, dim3(nz), dim3(256), 0, st, nz, nc, no, nv, nmo, a2, a4, ze, fs, fa, fb, acc);
+}
+void ediag(hipStream_t st, int nz, int O, int V, int nmo, int v0, const double* eps, const double* ze, double* acc) {
+  hipLaunchKernelGGL(k_ediag, dim3(nblocks(2L * nz * O * V)), dim3(256), 0, st, nz, O, V, nmo, v0, eps, ze, acc);
+}
+void xc_uks(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, int nmo,
+            const double* phi0, const double* phi1, const double* wfxc, double* U) {
+  const long waves = (long)G * nz;
+  const int blocks = (int)((waves * 64 + 255) / 256);
+  if (ncomp == 4)
+    hipLaunchKernelGGL(k_xc_uks<4>, dim3(blocks), dim3(256), 0, st, G, g0, ngrid, nz, O, nmo, phi0, phi1, wfxc, U);
+  else
+    hipLaunchKernelGGL(k_xc_uks<1>, dim3(blocks), dim3(256), 0, st, G, g0, ngrid, nz, O, nmo, phi0, phi1, wfxc, U);
+}
+void xc_sf(hipStream_t st, int G, int g0, int nz, int O, int nmo, const double* phio, const double* fsf, double* U) {
+  const long waves = (long)G * nz;
+  const int blocks = (int)((waves * 64 + 255) / 256);
+  hipLaunchKernelGGL(k_xc_sf, dim3(blocks), dim3(256), 0, st, G, g0, nz, O, nmo, phio, fsf, U);
+}
+void weight_fxc(hipStream_t st, long n4, int ngrid, const double* w, double* f) {
+  hipLaunchKernelGGL(k_weight_fxc, dim3(nblocks(n4 * ngrid)), dim3(256), 0, st, n4, ngrid, w, f);
+}
+void xsf_assemble(hipStream_t st, int nz, int nc, int no, int nv, int remove, const double* vects, const double* z, double* ze) {
+  const long n = (long)nz * (nc + no) * (no + nv);
+  hipLaunchKernelGGL(k_xsf_assemble, dim3(nblocks(n)), dim3(256), 0, st, nz, nc, no, nv, remove, vects, z, ze);
+}
+void xsf_extract(hipStream_t st, int nz, int nc, int no, int nv, int remove, const double* vects, const double* full, double* out) {
+  const long dim = (long)nc * nv + (long)nc * no + (long)no * nv + (long)no * no - (remove ? 1 : 0);
+  hipLaunchKernelGGL(k_xsf_extract, dim3(nblocks((long)nz * dim)), dim3(256), 0, st, nz, nc, no, nv, remove, vects, full, out);
+}
+void xsf_jdiag(hipStream_t st, int naux, int nmo, int nc, int no, int nv, const double* bmo, double* co_j, double* ov_j) {
+  const long n = (long)nc * no + (long)no * nv;
+  hipLaunchKernelGGL(k_xsf_jdiag, dim3(nblocks(n)), dim3(256), 0, st, naux, nmo, nc, no, nv, bmo, co_j, ov_j);
+}
+void precond(hipStream_t st, int nrow, int dim, const double* diag, const double* e, double shift, const double* r, double* out) {
+  hipLaunchKernelGGL(k_precond, dim3(nblocks((long)nrow * dim)), dim3(256), 0, st, nrow, dim, diag, e, shift, r, out);
+}
+void row_norms2(hipStream_t st, int nrow, int dim, const double* x, double* out) {
+  hipLaunchKernelGGL(k_row_norms2, dim3(nrow), dim3(256), 0, st, nrow, dim, x, out);
+}
+void row_scale(hipStream_t st, int nrow, int dim, double* x, const double* s) {
+  hipLaunchKernelGGL(k_row_scale, dim3(nblocks((long)nrow * dim)), dim3(256), 0, st, nrow, dim, x, s);
+}
+
+}  // namespace xt
