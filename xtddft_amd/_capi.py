@@ -52,6 +52,13 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise LibraryMissing(f"{LIB_PATH} not built; run xtddft_amd.build.build()")
+    # PyTorch-ROCm ships its own libamdhip64 (same SONAME).  Load it first so the
+    # library binds to that single HIP runtime instead of a second copy from
+    # /opt/rocm (two HIP/HSA runtimes in one process cannot share the device).
+    try:
+        import torch  # noqa: F401
+    except Exception:   # pragma: no cover -- plain C-ABI use without torch
+        pass
     try:
         L = ctypes.CDLL(LIB_PATH)
     except OSError as e:   # pragma: no cover

@@ -1,0 +1,174 @@
+"""Spin-adapted spin-flip TDA (XSF-TDA) with the reference's API
+(``xtddft/XSF_TDA.py``).
+
+``XSF_TDA(mf, SA=None, davidson=True, method=0, collinear_samples=60,
+calculate_sp=False)`` (XSF_TDA.py:146-213) and
+``kernel(nstates=1, remove=None, frozen=None, foo=1.0, d_lda=0.3,
+fglobal=None, fit=True)`` -> ``(e * 27.21138505, v)`` (XSF_TDA.py:1501-1554).
+
+* ``gen_tda_operation_sf(foo, fglobal)`` -> ``(vind, hdiag)`` (1029-1277):
+  the device operator (SF-down response + Fock + Delta-A of level ``SA``)
+  on cv|co|ov|oo vectors, OO compressed when ``remove``.
+* the preconditioner (915-961) takes its J diagonals from the device:
+  ``co_j[i,u] = sum_P B[P,i,u]^2`` -- one pass over the MO DF factor instead
+  of the reference's (nc*no + no*nv) unit-density J builds (859-913).
+* ``davidson_process`` uses the reference criteria tol 1e-8, lindep 1e-9,
+  max_cycle 1000 (1467-1470) on the device solver.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import scipy.linalg
+
+from . import davidson as _dav
+from .meanfield import MeanField
+from .operator import DeviceOperator
+from .sf_tda import _check_method, _dense, mf_info
+from .utils import HA2EV_XSF
+
+
+def get_vect(no):
+    """OO compression basis vects (no^2, no^2-1) (XSF_TDA.py:397-414)."""
+    tmp_v = np.zeros((no - 1, no))
+    for i in range(1, no):
+        factor = 1 / np.sqrt((no - i + 1) * (no - i))
+        tmp_v[i - 1][i - 1:] = np.array([no - i] + [-1] * (no - i)) * factor
+    vect = tmp_v.T
+    vects = np.eye(no * no)[:, :-1]
+    index = [0] + [i * (no + 1) for i in range(1, no)]
+    for i in range(vect.shape[1]):
+        vects[0::no + 1, index[i]] = vect[:, i]
+    return vects
+
+
+class XSF_TDA:
+    def __init__(self, mf: MeanField, SA=None, davidson=True, method=0, collinear_samples=60,
+                 calculate_sp=False, device=0, shard=(0, 1)):
+        _check_method(method)
+        self.mf = mf
+        self.type_u = not mf.is_rohf
+        self.SA = (0 if self.type_u else 3) if SA is None else SA
+        self.davidson = davidson
+        self.method = method
+        self.collinear_samples = collinear_samples
+        self.device = device
+        self.shard = shard
+        info = mf.shape_info()
+        self.nc, self.no, self.nv = info['nc'], info['no'], info['nv']
+        self.nocc_a, self.nocc_b = info['nocc_a'], info['nocc_b']
+        self.mo_energy, self.mo_occ, self.mo_coeff = mf_info(mf)
+        if mf.xctype == 'HF':
+            self.omega, self.alpha, self.hyb = 0.0, 0.0, 1.0
+        else:
+            self.omega, self.alpha, self.hyb = mf.omega, mf.alpha, mf.hyb
+        _, dsp1 = mf.spin_square()
+        self.ground_s = (dsp1 - 1) / 2
+        if calculate_sp:
+            raise NotImplementedError("spin-polarisation analysis (get_sp) is post-processing, out of scope")
+        self.re = None
+
+    # ------------------------------------------------------------ helpers
+    def get_vect(self):
+        return get_vect(self.no)
+
+    def default_fglobal(self, d_lda=0.3, fit=True):
+        cx = self.hyb if self.omega == 0 else self.hyb + (self.alpha - self.hyb) * math.erf(self.omega)
+        f = (1 - d_lda) * cx + d_lda
+        if self.method == 1 and fit:
+            f = f * 4 * (cx - 0.5) ** 2
+        return f
+
+    def _operator(self, foo, fglobal):
+        op = DeviceOperator(self.mf, 'XSF', sa=self.SA, foo=foo, fglobal=fglobal, remove=bool(self.re),
+                            device=self.device, shard=self.shard)
+        if self.re:
+            op.set_oo_basis(self.vects)
+        return op
+
+    def _build_preconditioner_hdiag(self, fglobal, op):
+        mf = self.mf
+        fockA, fockB = mf.fock_mo()
+        nc, no = self.nc, self.no
+        si = no / 2.0
+        hdiag = fockB.diagonal()[self.nocc_b:][None, :] - fockA.diagonal()[:self.nocc_a, None]
+        if self.SA > 0:
+            fa_hf, fb_hf = mf.fock_mo_hf()
+            diag_s = ((fb_hf - fa_hf) * 0.5).diagonal()
+            co_j, ov_j = op.xsf_j_diagonals()
+            hdiag[:nc, no:] += fglobal * (diag_s[nc + no:] + diag_s[:nc, None]) / si
+            hdiag[:nc, :no] += fglobal * (2.0 * diag_s[:nc, None] - co_j) / (2 * si - 1)
+            hdiag[nc:, no:] += fglobal * (2.0 * diag_s[nc + no:] - ov_j) / (2 * si - 1)
+        return np.hstack([hdiag[:nc, no:].ravel(), hdiag[:nc, :no].ravel(),
+                          hdiag[nc:, no:].ravel(), hdiag[nc:, :no].ravel()])
+
+    def _compress_removed_hdiag(self, hdiag):
+        d3 = self.nc * self.nv + self.nc * self.no + self.no * self.nv
+        out = np.empty(hdiag.size - 1)
+        out[:d3] = hdiag[:d3]
+        out[d3:] = np.einsum("x,xy,xy->y", hdiag[d3:], self.vects, self.vects)
+        return out
+
+    def gen_tda_operation_sf(self, foo=1.0, fglobal=None):
+        if self.re is None:
+            self.re = not self.type_u
+        if self.re:
+            self.vects = self.get_vect()
+        if fglobal is None:
+            fglobal = self.default_fglobal()
+        op = self._operator(foo, fglobal)
+        hdiag = self._build_preconditioner_hdiag(fglobal, op)
+        if self.re:
+            hdiag = self._compress_removed_hdiag(hdiag)
+
+        def vind(zs0):
+            if isinstance(zs0, (list, tuple)):
+                zs0 = np.asarray(zs0)
+            return op.apply(zs0)
+        vind.operator = op
+        return vind, hdiag
+
+    def init_guess(self, nstates, hdiag):
+        gaps = np.asarray(hdiag)
+        nroots = min(nstates, gaps.size)
+        if nroots < 1:
+            raise ValueError("No spin-flip excitation space is available.")
+        thr = np.sort(gaps)[nroots - 1] + 1e-5
+        idx = np.where(gaps <= thr)[0]
+        x0 = np.zeros((idx.size, gaps.size))
+        x0[np.arange(idx.size), idx] = 1.0
+        return x0
+
+    def davidson_process(self, foo, fglobal):
+        vind, hdiag = self.gen_tda_operation_sf(foo, fglobal)
+        x0 = self.init_guess(self.nstates, hdiag)
+        self.converged, self.e, x1, self.icyc = _dav.davidson1(
+            vind, x0, hdiag, tol=1e-8, lindep=1e-9, nroots=self.nstates, max_cycle=1000,
+            device=self.device)
+        self.v = np.array(x1).T
+
+    def get_Amat(self, foo=1.0, fglobal=None):
+        """Explicit (remove-compressed when self.re) A through the device operator."""
+        vind, _ = self.gen_tda_operation_sf(foo, fglobal)
+        return _dense(vind.operator)
+
+    def kernel(self, nstates=1, remove=None, frozen=None, foo=1.0, d_lda=0.3, fglobal=None, fit=True):
+        if frozen is not None:
+            raise NotImplementedError("frozen-orbital XSF (frozen_A) is outside the hot path")
+        self.re = (not self.type_u) if remove is None else bool(remove)
+        if self.re and self.no < 2:
+            raise ValueError("OO compression needs at least two open shells")
+        nov = (self.nc + self.no) * (self.no + self.nv)
+        self.nstates = min(nstates, nov)
+        if fglobal is None:
+            fglobal = self.default_fglobal(d_lda, fit)
+        self.fglobal = fglobal
+        if self.davidson:
+            self.davidson_process(foo=foo, fglobal=fglobal)
+        else:
+            self.A = self.get_Amat(foo=foo, fglobal=fglobal)
+            e, v = scipy.linalg.eigh(self.A)
+            self.e = e[:self.nstates]
+            self.v = v[:, :self.nstates]
+        return np.asarray(self.e) * HA2EV_XSF, self.v
