@@ -98,6 +98,12 @@ int xt_dim(const xt_ctx* ctx);
 /* per-phase device timings of the last xt_apply (ms): jk, xc, local, total */
 int xt_last_timings(const xt_ctx* ctx, double* out4);
 
+/* live timing of GEMM classes (mask bit t: t = 1 DF exchange contraction, 2 XC grid
+   forward, 3 XC back-projection; 0 = off); xt_profile_stats(tag): {device ms summed over the
+   launches of the last xt_apply, number of launches, algorithmic flops} */
+int xt_set_profile(xt_ctx* ctx, int tag);
+int xt_profile_stats(const xt_ctx* ctx, int tag, double* out3);
+
 /* XSF preconditioner J diagonals (XSF_TDA.py:859-913): co_j (nc x no), ov_j (no x nv). */
 int xt_xsf_j_diagonals(xt_ctx* ctx, double* co_j, double* ov_j, int ptr_kind);
 

@@ -24,7 +24,7 @@ EXPORTS = [
     "xt_create", "xt_destroy", "xt_set_stream", "xt_last_error", "xt_abi_version",
     "xt_set_orbitals", "xt_set_fock_mo", "xt_set_orbital_energies", "xt_set_jk_df",
     "xt_set_grid", "xt_set_oo_basis", "xt_apply", "xt_dim", "xt_last_timings",
-    "xt_xsf_j_diagonals", "xt_dgemm", "xt_precond", "xt_row_norms2", "xt_row_scale",
+    "xt_xsf_j_diagonals", "xt_set_profile", "xt_profile_stats", "xt_dgemm", "xt_precond", "xt_row_norms2", "xt_row_scale",
 ]
 
 
@@ -79,6 +79,8 @@ def lib():
     L.xt_dim.argtypes = [vp]
     L.xt_last_timings.argtypes = [vp, dp]
     L.xt_xsf_j_diagonals.argtypes = [vp, dp, dp, c_int]
+    L.xt_set_profile.argtypes = [vp, c_int]
+    L.xt_profile_stats.argtypes = [vp, c_int, dp]
     L.xt_dgemm.argtypes = [c_int, c_int, c_int, c_int, c_int, c_double, dp, c_long, dp, c_long,
                            c_double, dp, c_long, vp]
     L.xt_precond.argtypes = [c_int, c_int, dp, dp, c_double, dp, dp, vp]

@@ -65,6 +65,14 @@ struct xt_ctx {
   DevBuf ze, acc, kx, zr, tbuf, ubuf, gam, gam2, ws, stage, stage2, zin, sout, trace;
   hipEvent_t ev[5];
   double timings[4] = {0, 0, 0, 0};
+  // live per-kernel timing of tagged GEMM classes (bench roofline); mask bit t = tag t
+  int prof_mask = 0;
+  std::vector<hipEvent_t> pev;     // pairs
+  std::vector<int> pev_tag;
+  int pev_used = 0;
+  double prof_flops[4] = {0, 0, 0, 0};
+  double prof_ms[4] = {0, 0, 0, 0};
+  int prof_launches[4] = {0, 0, 0, 0};
 };
 
 static int dim_of(const xt_desc& d) {
@@ -86,6 +94,19 @@ static int to_device(xt_ctx* c, DevBuf& dst, const double* src, size_t count, in
 }
 
 static int gemm(xt_ctx* c, const GemmDesc& g) {
+  const bool prof = g.tag > 0 && g.tag < 4 && ((c->prof_mask >> g.tag) & 1);
+  if (prof) {
+    if ((int)c->pev.size() < c->pev_used + 2) {
+      hipEvent_t a, b;
+      HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
+      c->pev.push_back(a); c->pev.push_back(b);
+      c->pev_tag.push_back(0); c->pev_tag.push_back(0);
+    }
+    c->pev_tag[c->pev_used] = g.tag;
+    HIPCHK(hipEventRecord(c->pev[c->pev_used], c->st));
+    c->prof_flops[g.tag] += 2.0 * g.M * (double)g.N * g.K * (g.R > 0 ? g.R : 1) *
+                            (g.nb1 > 0 ? g.nb1 : 1) * (g.nb2 > 0 ? g.nb2 : 1);
+  }
   size_t need = dgemm_workspace_bytes(g);
   if (need > 0) {
     size_t cap = (size_t)512 << 20;   // 512 MiB split-K workspace cap
@@ -94,10 +115,30 @@ static int gemm(xt_ctx* c, const GemmDesc& g) {
   }
   int r = dgemm(g, c->st, c->ws.p, c->ws.n * sizeof(double));
   if (r) return fail(r, "dgemm launch failed");
+  if (prof) {
+    HIPCHK(hipEventRecord(c->pev[c->pev_used + 1], c->st));
+    c->pev_used += 2;
+    c->prof_launches[g.tag] += 1;
+  }
   return 0;
 }
 
 extern "C" {
+
+int xt_set_profile(xt_ctx* c, int mask) {
+  if (!c) return fail(XT_ERR_ARG, "null ctx");
+  c->prof_mask = mask;
+  return 0;
+}
+
+// device ms, launches and algorithmic flops of GEMM class `tag` in the last
+// xt_apply (one launch = one GEMM call including its split-K reduce)
+int xt_profile_stats(const xt_ctx* c, int tag, double* out3) {
+  if (!c || !out3 || tag < 1 || tag > 3) return fail(XT_ERR_ARG, "bad argument");
+  out3[0] = c->prof_ms[tag]; out3[1] = c->prof_launches[tag]; out3[2] = c->prof_flops[tag];
+  return 0;
+}
+
 
 int xt_abi_version(void) { return XT_ABI_VERSION; }
 const char* xt_last_error(void) { return g_err.c_str(); }
@@ -158,6 +199,7 @@ int xt_destroy(xt_ctx* c) {
                     &c->stage, &c->stage2, &c->zin, &c->sout, &c->trace};
   for (DevBuf* b : bufs) b->release();
   for (int i = 0; i < 5; ++i) (void)hipEventDestroy(c->ev[i]);
+  for (hipEvent_t e : c->pev) (void)hipEventDestroy(e);
   delete c;
   return 0;
 }
@@ -371,6 +413,7 @@ static int sandwich(xt_ctx* c, const double* Bo, const double* Bv, int nz,
       g2.B = Bv + p0 * mm + (long)cx0 * nmo + cy0; g2.sBk = nmo; g2.sBn = 1; g2.sBr = mm;
       g2.C = c->kx.p; g2.ldc = ncy;
       g2.alpha = 1.0; g2.beta = (p0 == 0) ? 0.0 : 1.0;
+      g2.tag = 1;
       RET(gemm(c, g2));
     }
     // S[x][j][b] += coef * kx[j][x][b]
@@ -475,6 +518,7 @@ static int xc_response(xt_ctx* c, int nz) {
       g.A = c->Phi.p + c->vir_basis[ch] * basP + (long)g0 * nmo + c->v0; g.sAm = nmo; g.sAk = 1; g.sAb1 = compP;
       g.B = c->ze.p + ch * chs; g.sBn = V; g.sBk = 1;
       g.C = c->ubuf.p + ch * chU; g.ldc = ldU; g.sCb1 = compU;
+      g.tag = 2;
       RET(gemm(c, g));
     }
     if (nch == 2) {
@@ -489,6 +533,7 @@ static int xc_response(xt_ctx* c, int nz) {
       g.A = c->ubuf.p + ch * chU; g.sAm = 1; g.sAk = ldU; g.sAr = compU;
       g.B = c->Phi.p + c->vir_basis[ch] * basP + (long)g0 * nmo + c->v0; g.sBk = nmo; g.sBn = 1; g.sBr = compP;
       g.C = c->acc.p + ch * chs; g.ldc = V; g.beta = 1.0;
+      g.tag = 3;
       RET(gemm(c, g));
     }
   }
@@ -611,6 +656,8 @@ extern "C" int xt_apply(xt_ctx* c, int nz, const double* z, double* sigma, int p
   }
   RET(c->ze.ensure(nch * chs));
   RET(c->acc.ensure(nch * chs));
+  c->pev_used = 0;
+  for (int t = 0; t < 4; ++t) { c->prof_flops[t] = 0.0; c->prof_ms[t] = 0.0; c->prof_launches[t] = 0; }
   HIPCHK(hipEventRecord(c->ev[0], c->st));
   // ---- embed trial vectors -------------------------------------------------
   if (d.kind == XT_KIND_XTDA || d.kind == XT_KIND_UTDA) embed_xtda(c->st, nz, d.nc, d.no, d.nv, zd, c->ze.p);
@@ -706,6 +753,11 @@ extern "C" int xt_apply(xt_ctx* c, int nz, const double* z, double* sigma, int p
   (void)hipEventElapsedTime(&t23, c->ev[2], c->ev[3]);
   (void)hipEventElapsedTime(&t04, c->ev[0], c->ev[4]);
   c->timings[0] = t12; c->timings[1] = t23; c->timings[2] = t01; c->timings[3] = t04;
+  for (int i = 0; i < c->pev_used; i += 2) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, c->pev[i], c->pev[i + 1]);
+    c->prof_ms[c->pev_tag[i]] += ms;
+  }
   if (ptr_kind == XT_PTR_HOST) HIPCHK(hipStreamSynchronize(c->st));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(XT_ERR_HIP, std::string("kernel error: ") + hipGetErrorString(e));

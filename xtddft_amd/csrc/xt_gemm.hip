@@ -40,7 +40,9 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int BK = 16;
 constexpr int LDP = 18;          // LDS row pitch in doubles (16 + 2 pad, keeps 16-B alignment)
 
-template <int BM, int BN, int WGM, int WGN, bool A_KC, bool B_KC>
+// TAG only gives hot call sites their own kernel symbol (rocprofv3 identity):
+// 1 = DF-exchange contraction, 2 = XC grid forward, 3 = XC grid back-projection.
+template <int BM, int BN, int WGM, int WGN, bool A_KC, bool B_KC, int TAG>
 __global__ void __launch_bounds__(64 * WGM * WGN, 2)
 dgemm_kernel(GemmParams p) {
   constexpr int NTHREADS = 64 * WGM * WGN;
@@ -219,15 +221,25 @@ __global__ void splitk_reduce(GemmParams p) {
   }
 }
 
-template <int BM, int BN, int WGM, int WGN>
-static void launch_cfg(const GemmParams& p, hipStream_t st, bool akc, bool bkc) {
+template <int BM, int BN, int WGM, int WGN, int TAG>
+static void launch_tag(const GemmParams& p, hipStream_t st, bool akc, bool bkc) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   dim3 grid(tiles, 1, p.nbatch * p.nsplit);
   dim3 block(64 * WGM * WGN);
-  if (akc && bkc)  hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, true, true>), grid, block, 0, st, p);
-  else if (akc)    hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, true, false>), grid, block, 0, st, p);
-  else if (bkc)    hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, false, true>), grid, block, 0, st, p);
-  else             hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, false, false>), grid, block, 0, st, p);
+  if (akc && bkc)  hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, true, true, TAG>), grid, block, 0, st, p);
+  else if (akc)    hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, true, false, TAG>), grid, block, 0, st, p);
+  else if (bkc)    hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, false, true, TAG>), grid, block, 0, st, p);
+  else             hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, false, false, TAG>), grid, block, 0, st, p);
+}
+
+template <int BM, int BN, int WGM, int WGN>
+static void launch_cfg(const GemmParams& p, hipStream_t st, bool akc, bool bkc, int tag) {
+  if (BM == 128 && BN == 128) {
+    if (tag == 1) { launch_tag<BM, BN, WGM, WGN, 1>(p, st, akc, bkc); return; }
+    if (tag == 2) { launch_tag<BM, BN, WGM, WGN, 2>(p, st, akc, bkc); return; }
+    if (tag == 3) { launch_tag<BM, BN, WGM, WGN, 3>(p, st, akc, bkc); return; }
+  }
+  launch_tag<BM, BN, WGM, WGN, 0>(p, st, akc, bkc);
 }
 
 size_t dgemm_workspace_bytes(const GemmDesc& d) {
@@ -291,10 +303,10 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
     }
     p.ws = ws;
   }
-  if (bm == 128 && bn == 128)      launch_cfg<128, 128, 2, 4>(p, st, akc, bkc);
-  else if (bm == 128)              launch_cfg<128, 64, 2, 2>(p, st, akc, bkc);
-  else if (bn == 128)              launch_cfg<64, 128, 2, 2>(p, st, akc, bkc);
-  else                             launch_cfg<64, 64, 2, 2>(p, st, akc, bkc);
+  if (bm == 128 && bn == 128)      launch_cfg<128, 128, 2, 4>(p, st, akc, bkc, d.tag);
+  else if (bm == 128)              launch_cfg<128, 64, 2, 2>(p, st, akc, bkc, d.tag);
+  else if (bn == 128)              launch_cfg<64, 128, 2, 2>(p, st, akc, bkc, d.tag);
+  else                             launch_cfg<64, 64, 2, 2>(p, st, akc, bkc, d.tag);
   if (p.nsplit > 1) {
     long total = (long)p.nbatch * p.M * p.N;
     int blocks = (int)((total + 255) / 256);

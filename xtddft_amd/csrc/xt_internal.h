@@ -24,6 +24,7 @@ struct GemmDesc {
   long ldc = 0, sCb1 = 0, sCb2 = 0;
   double alpha = 1.0, beta = 0.0;
   int max_split = 0;                  // 0 = heuristic
+  int tag = 0;                        // kernel identity for profiling (see xt_gemm.hip)
 };
 
 struct GemmParams {

@@ -69,7 +69,8 @@ def shape_info(mf: MeanField, kind: str):
 class DeviceOperator:
     def __init__(self, mf: MeanField, kind: str, *, sa: int = 0, foo: float = 1.0,
                  fglobal: float = 0.0, remove: bool = False, shard=(0, 1), device: int = 0,
-                 stream=None):
+                 stream=None, presharded: bool = False):
+        """presharded: mf.cderi / mf.grids already hold only this rank's slice."""
         L = _capi.lib()
         self.mf, self.kind = mf, kind
         rank, nranks = shard
@@ -77,9 +78,12 @@ class DeviceOperator:
         nmo = nc + no + nv
         self.nc, self.no, self.nv = nc, no, nv
         naux = mf.naux
-        self.aux_range = _split(naux, rank, nranks)
         ngrid = mf.grids.ngrid if (mf.grids is not None and mf.xctype != "HF") else 0
-        self.grid_range = _split(ngrid, rank, nranks)
+        if presharded:
+            self.aux_range, self.grid_range = (0, naux), (0, ngrid)
+        else:
+            self.aux_range = _split(naux, rank, nranks)
+            self.grid_range = _split(ngrid, rank, nranks)
         d = _capi.XtDesc()
         d.kind = _capi.KIND[kind]
         d.restricted = 1 if mf.is_rohf else 0
@@ -180,6 +184,20 @@ class DeviceOperator:
         buf = (ctypes.c_double * 4)()
         _capi.check(self._L.xt_last_timings(self._h, ctypes.cast(buf, ctypes.c_void_p)), "timings")
         return dict(jk_ms=buf[0], xc_ms=buf[1], local_ms=buf[2], total_ms=buf[3])
+
+    PROFILE_TAGS = {1: "df_exchange_contract", 2: "xc_grid_forward", 3: "xc_grid_back"}
+
+    def set_profile(self, mask: int = 0b1110):
+        """Time GEMM classes live with HIP events (bit 1 exchange, 2 XC forward, 3 XC back)."""
+        _capi.check(self._L.xt_set_profile(self._h, int(mask)), "xt_set_profile")
+
+    def profile_stats(self):
+        out = {}
+        for tag, name in self.PROFILE_TAGS.items():
+            buf = (ctypes.c_double * 3)()
+            _capi.check(self._L.xt_profile_stats(self._h, tag, ctypes.cast(buf, ctypes.c_void_p)), "stats")
+            out[name] = dict(tag=tag, ms=buf[0], launches=int(buf[1]), flops=buf[2])
+        return out
 
     def xsf_j_diagonals(self):
         co = np.empty((self.nc, self.no))

@@ -164,6 +164,68 @@ def make_mf(nao=24, nc=5, no=2, naux=None, ngrid=None, xctype="GGA", hyb=0.2,
                      omega=omega, alpha=alpha, hyb=hyb)
 
 
+def make_device_mf(nao=1000, nc=99, no=2, naux=None, ngrid=None, xctype="GGA", hyb=0.2,
+                   seed=DEFAULT_SEED, device=0, shard=(0, 1)) -> MeanField:
+    """Synthetic ROKS problem whose big tensors are generated directly in HBM.
+
+    Same distributions as ``make_mf`` (torch RNG, so not bitwise equal): the
+    DF factor and the grid are generated only for this rank's shard
+    (aux rows / grid points ``shard = (rank, nranks)``), scaled with the
+    GLOBAL sizes so every shard count describes the same operator statistics.
+    Small per-orbital data (C, Fock, energies) come from ``make_mf`` and are
+    identical on every rank.
+    """
+    import torch
+    naux = naux if naux is not None else 3 * nao
+    ngrid = ngrid if ngrid is not None else 1200 * nao
+    rank, nranks = shard
+    small = make_mf(nao=nao, nc=nc, no=no, naux=1, ngrid=1, xctype=xctype, hyb=hyb, seed=seed)
+    dev = torch.device(f"cuda:{device}")
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed + 7919 * (rank + 1))
+    nv = nao - nc - no
+
+    def split(n):
+        base, rem = divmod(n, nranks)
+        lo = rank * base + min(rank, rem)
+        return lo, lo + base + (1 if rank < rem else 0)
+    p0, p1 = split(naux)
+    g0, g1 = split(ngrid)
+    nocc, nvir = nc + no, no + nv
+    k = torch.arange(nao, device=dev, dtype=torch.float64)
+    dmat = torch.exp(-torch.abs(k[:, None] - k[None, :]) / 50.0)
+    s = df_scale(nao, naux, nocc, nvir) / np.sqrt(2.0)
+    cderi = torch.empty((p1 - p0, nao, nao), dtype=torch.float64, device=dev)
+    for q0 in range(0, p1 - p0, 64):
+        q1 = min(p1 - p0, q0 + 64)
+        t = torch.randn((q1 - q0, nao, nao), dtype=torch.float64, device=dev, generator=g)
+        cderi[q0:q1] = (t + t.transpose(1, 2)) * s * dmat
+        del t
+    ncomp = 4 if xctype == "GGA" else 1
+    ng = g1 - g0
+    scale = grid_scale(ngrid, nocc, nvir)
+    ao = torch.randn((ncomp, ng, nao), dtype=torch.float64, device=dev, generator=g)
+    ao.mul_(scale)
+    w = torch.rand(ng, dtype=torch.float64, device=dev, generator=g) / ngrid
+    n = 2 * ncomp
+    f = torch.randn((n, n, ng), dtype=torch.float64, device=dev, generator=g) * 0.01
+    f = 0.5 * (f + f.transpose(0, 1))
+    for sa in range(2):
+        for sb in range(2):
+            v = -(0.1 + 0.9 * torch.rand(ng, dtype=torch.float64, device=dev, generator=g))
+            f[sa * ncomp, sb * ncomp] = v
+            f[sb * ncomp, sa * ncomp] = v
+    fxc = f.reshape(2, ncomp, 2, ncomp, ng).contiguous()
+    fxc_sf = -(0.1 + 0.9 * torch.rand(ng, dtype=torch.float64, device=dev, generator=g)) * w
+    small.cderi = cderi
+    small.grids = Grid(ao=ao, weights=w)
+    small.fxc = fxc
+    small.fxc_sf = fxc_sf
+    small.extra = dict(shard=shard, aux_range=(p0, p1), grid_range=(g0, g1), naux_global=naux,
+                       ngrid_global=ngrid)
+    return small
+
+
 def make_trial_vectors(nz, dim, seed=DEFAULT_SEED + 1):
     """Row-normalised N(0,1) trial vectors."""
     rng = np.random.default_rng(seed)
