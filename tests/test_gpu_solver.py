@@ -1,0 +1,112 @@
+"""GPU: the FP64-MFMA GEMM engine, the device Davidson and the reference-style
+drivers, plus size-independent properties at larger sizes."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import davidson as odav
+from oracle import sf_tda as osf
+from oracle import xsf_tda as oxsf
+from oracle import xtda as oxtda
+from xtddft_amd.synthetic import make_mf, make_trial_vectors
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch(hiplib):
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch
+
+
+@pytest.mark.parametrize("m,n,k", [(1, 1, 1), (17, 33, 5), (128, 128, 16), (200, 301, 257),
+                                   (40, 7, 100000), (513, 129, 64), (3, 1000, 0)])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_dgemm_layouts(torch, hiplib, m, n, k, ta, tb):
+    from xtddft_amd import _capi
+    g = torch.Generator(device="cuda").manual_seed(m * 7 + n * 13 + k)
+    a = torch.randn((k, m) if ta else (m, k), dtype=torch.float64, device="cuda", generator=g)
+    b = torch.randn((n, k) if tb else (k, n), dtype=torch.float64, device="cuda", generator=g)
+    c = torch.randn((m, n), dtype=torch.float64, device="cuda", generator=g)
+    ref = 0.7 * ((a.T if ta else a) @ (b.T if tb else b)) - 0.3 * c
+    st = torch.cuda.current_stream().cuda_stream
+    _capi.check(hiplib.xt_dgemm(ta, tb, m, n, k, 0.7, a.data_ptr(), a.shape[1], b.data_ptr(),
+                                b.shape[1], -0.3, c.data_ptr(), n, ctypes.c_void_p(st)), "dgemm")
+    torch.cuda.synchronize()
+    scale = max(1.0, float(ref.abs().max()))
+    assert float((c - ref).abs().max()) / scale < 1e-13 * max(1, k) ** 0.5
+
+
+def test_davidson_matches_oracle_davidson(torch):
+    from xtddft_amd.davidson import DiagPrecond, davidson1
+    from xtddft_amd.operator import DeviceOperator
+    mf = make_mf(nao=40, nc=8, no=2, xctype="GGA", hyb=0.2)
+    vind, hdiag = oxtda.gen_tda_operation(mf)
+    x0 = oxtda.get_init_guess(mf, 8)
+    # (tol_residual 1e-7 with lindep 1e-12 makes the reference algorithm exit early on
+    #  linear dependence -- both solvers do -- so the comparison runs at 1e-6)
+    c1, e1, _, _ = odav.davidson1(vind, x0, oxtda.get_precond(mf, hdiag), tol_residual=1e-6,
+                                  lindep=1e-12, nroots=8, pick=oxtda.pickeig, max_cycle=100)
+    op = DeviceOperator(mf, "XTDA")
+    c2, e2, x2, _ = davidson1(op.apply, x0, DiagPrecond(hdiag, 0.0), tol_residual=1e-6, lindep=1e-12,
+                              nroots=8, pick=oxtda.pickeig, max_cycle=100)
+    assert c1.all() and c2.all()
+    assert np.abs(e1 - e2).max() < 1e-9
+    x2 = np.asarray(x2)
+    assert np.allclose(x2 @ x2.T, np.eye(8), atol=1e-8)
+
+
+def test_xtda_driver_davidson_and_full_diag(torch):
+    from xtddft_amd import XTDA
+    mf = make_mf(nao=36, nc=7, no=2, xctype="GGA", hyb=0.2)
+    vind, hdiag = oxtda.gen_tda_operation(mf)
+    w = np.linalg.eigvalsh(vind(np.eye(hdiag.size)).T)
+    x = XTDA(mf.mol, mf, nstates=6)
+    e = x.kernel()
+    assert x.converged.all() and np.abs(e - w[:6]).max() < 1e-9
+    assert x.v.shape == (hdiag.size, 6) and x.dS2.shape == (6,)
+    y = XTDA(mf.mol, mf, nstates=6, use_Davidson=False)
+    assert np.abs(y.kernel() - w[:6]).max() < 1e-12
+    lines = y.analyze(verbose=False)
+    assert lines[0].startswith("D1")
+
+
+def test_sf_and_xsf_drivers(torch):
+    from xtddft_amd import SF_TDA, XSF_TDA
+    mf = make_mf(nao=36, nc=7, no=3, xctype="GGA", hyb=0.5)
+    for isf in (-1, 1):
+        e, v = SF_TDA(mf, isf=isf).kernel(nstates=4)
+        vind, hdiag = osf.gen_tda_operation_sf(mf, isf)
+        w = np.linalg.eigvalsh(vind(np.eye(hdiag.size)).T)
+        assert np.abs(e - w[:4] * 27.2113834).max() < 1e-5       # tol 1e-7 (SF_TDA.py:392)
+        e2, _ = SF_TDA(mf, isf=isf, davidson=False).kernel(nstates=4)
+        assert np.abs(e2 - w[:4] * 27.2113834).max() < 1e-9
+    x = XSF_TDA(mf)
+    e, v = x.kernel(nstates=5)
+    o = oxsf.XSFOracle(mf)
+    vind, hdiag = o.gen_tda_operation_sf()
+    w = np.linalg.eigvalsh(vind(np.eye(hdiag.size)).T)
+    assert x.converged.all() and np.abs(e - w[:5] * 27.21138505).max() < 1e-5
+    e2, _ = XSF_TDA(mf, davidson=False).kernel(nstates=5)
+    assert np.abs(e2 - w[:5] * 27.21138505).max() < 1e-9
+
+
+@pytest.mark.parametrize("kind", ["XTDA", "SF_DOWN"])
+def test_properties_at_larger_size(torch, kind):
+    """Symmetry <y, A x> = <A y, x> and linearity at nao = 240 (oracle too slow here)."""
+    from xtddft_amd.operator import DeviceOperator
+    mf = make_mf(nao=240, nc=40, no=2, naux=600, ngrid=20000, xctype="GGA", hyb=0.3,
+                 omega=0.3, alpha=0.6)
+    op = DeviceOperator(mf, kind)
+    x = make_trial_vectors(4, op.dim, seed=1)
+    y = make_trial_vectors(4, op.dim, seed=2)
+    ax, ay = op.apply(x), op.apply(y)
+    lhs, rhs = y @ ax.T, ay @ x.T
+    assert np.abs(lhs - rhs).max() < 1e-12 * np.abs(lhs).max()
+    comb = op.apply(0.3 * x - 1.7 * y)
+    assert np.abs(comb - (0.3 * ax - 1.7 * ay)).max() < 1e-12 * np.abs(comb).max()
+    # the batch size does not change a vector's image
+    single = op.apply(x[2:3])
+    assert np.abs(single - ax[2:3]).max() < 1e-13 * np.abs(single).max()

@@ -1,0 +1,125 @@
+"""CPU: host-side logic of the framework (no GPU, no compute calls)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import sf_tda as osf
+from oracle import xsf_tda as oxsf
+from oracle import xtda as oxtda
+from xtddft_amd import meanfield, parallel, utils
+from xtddft_amd.synthetic import make_mf
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "xtddft_amd.h")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(xt_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_builds_and_exports_every_header_symbol(hiplib):
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(hiplib, s), s
+    assert hiplib.xt_abi_version() == 1
+
+
+def test_desc_layout_matches_c_header(tmp_path):
+    """ctypes XtDesc has the same size/offsets as the C struct (gcc on the header)."""
+    from xtddft_amd._capi import XtDesc
+    fields = [f for f, _ in XtDesc._fields_]
+    src = tmp_path / "t.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "xtddft_amd.h"\nint main(){'
+                   'printf("%zu", sizeof(xt_desc));' +
+                   "".join(f'printf(" %zu", offsetof(xt_desc, {f}));' for f in fields) + "return 0;}")
+    exe = tmp_path / "t"
+    subprocess.check_call(["gcc", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)])
+    out = [int(v) for v in subprocess.check_output([str(exe)]).split()]
+    assert out[0] == ctypes.sizeof(XtDesc)
+    assert out[1:] == [getattr(XtDesc, f).offset for f in fields]
+
+
+def test_create_rejects_bad_descriptor_without_gpu(hiplib):
+    """Argument validation happens before any HIP call (reference ValueError, XTDA.py:37)."""
+    from xtddft_amd import _capi
+    d = _capi.XtDesc(kind=0, restricted=1, nao=10, nmo=10, nc=3, no=2, nv=4)   # nc+no+nv != nmo
+    h = ctypes.c_void_p()
+    rc = hiplib.xt_create(ctypes.byref(d), ctypes.byref(h))
+    assert rc == -1
+    with pytest.raises(ValueError):
+        _capi.check(rc, "xt_create")
+    d = _capi.XtDesc(kind=0, restricted=0, nao=10, nmo=10, nc=3, no=2, nv=5, si=1.0)  # XTDA needs ROKS
+    assert hiplib.xt_create(ctypes.byref(d), ctypes.byref(h)) == -1
+    d = _capi.XtDesc(kind=4, restricted=1, nao=10, nmo=10, nc=3, no=1, nv=6, sa=3)   # 2S-1 = 0
+    assert hiplib.xt_create(ctypes.byref(d), ctypes.byref(h)) == -1
+    assert b"2S-1" in hiplib.xt_last_error()
+
+
+def test_meanfield_requires_core_open_virtual_order():
+    mf = make_mf(nao=10, nc=2, no=2)
+    occ = mf.mo_occ.copy()
+    occ[[1, 2]] = occ[[2, 1]]
+    with pytest.raises(ValueError):
+        meanfield.MeanField(mol=mf.mol, mo_coeff=mf.mo_coeff, mo_occ=occ, mo_energy=mf.mo_energy,
+                            h1e=mf.h1e, veff=mf.veff, veff_hf=mf.veff_hf, cderi=mf.cderi)
+
+
+def test_synthetic_is_seeded():
+    a = make_mf(nao=12, nc=3, no=2, seed=5)
+    b = make_mf(nao=12, nc=3, no=2, seed=5)
+    assert np.array_equal(a.cderi, b.cderi) and np.array_equal(a.grids.ao, b.grids.ao)
+
+
+def test_product_init_guess_and_hdiag_match_oracle():
+    from xtddft_amd.xtda import XTDA
+    for kind in ("RO", "U"):
+        mf = make_mf(nao=16, nc=4, no=2, kind=kind)
+        x = XTDA(mf.mol, mf, nstates=5)
+        vind, hdiag = oxtda.gen_tda_operation(mf)
+        assert np.abs(x._hdiag() - hdiag).max() == 0
+        assert np.array_equal(x.get_init_guess(mf, 5), oxtda.get_init_guess(mf, 5))
+        pre = oxtda.get_precond(mf, hdiag)
+        r = np.random.default_rng(0).standard_normal(hdiag.size)
+        assert np.allclose(pre(r.copy(), 0.3), r / (hdiag - 0.3))
+
+
+def test_sf_and_xsf_host_pieces_match_oracle():
+    from xtddft_amd import sf_tda, xsf_tda
+    mf = make_mf(nao=16, nc=4, no=3, xctype="GGA", hyb=0.5)
+    for isf in (-1, 1):
+        assert np.array_equal(sf_tda.init_guess(mf, 4, isf), osf.init_guess(mf, 4, isf))
+    for no in (2, 3, 4):
+        v = xsf_tda.get_vect(no)
+        assert np.array_equal(v, oxsf.get_vect(no))
+        assert np.allclose(v.T @ v, np.eye(no * no - 1))
+    x = xsf_tda.XSF_TDA.__new__(xsf_tda.XSF_TDA)
+    x.hyb, x.alpha, x.omega, x.method = 0.5, 0.0, 0.0, 0
+    assert abs(x.default_fglobal() - oxsf.default_fglobal(mf)) < 1e-15
+
+
+def test_so2st_roundtrip():
+    v = np.random.default_rng(1).standard_normal((3 * 5 + 2 * 5 + 3 * 2 + 3 * 5, 4))
+    assert np.allclose(utils.st2so(utils.so2st(v, 3, 2, 5), 3, 2, 5), v)
+
+
+def test_shard_ranges_cover_exactly():
+    for n in (1, 7, 3000, 1200000):
+        for nr in (1, 2, 3, 8):
+            rs = [parallel.shard_range(n, r, nr) for r in range(nr)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(nr - 1))
+
+
+def test_no_cpu_fallback_in_product():
+    """The product package never imports the oracle (test infrastructure only)."""
+    pkg = os.path.join(ROOT, "xtddft_amd")
+    for f in os.listdir(pkg):
+        if f.endswith(".py"):
+            src = open(os.path.join(pkg, f)).read()
+            assert "import oracle" not in src and "from oracle" not in src, f

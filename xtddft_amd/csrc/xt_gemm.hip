@@ -234,12 +234,10 @@ static void launch_tag(const GemmParams& p, hipStream_t st, bool akc, bool bkc) 
 
 template <int BM, int BN, int WGM, int WGN>
 static void launch_cfg(const GemmParams& p, hipStream_t st, bool akc, bool bkc, int tag) {
-  if (BM == 128 && BN == 128) {
-    if (tag == 1) { launch_tag<BM, BN, WGM, WGN, 1>(p, st, akc, bkc); return; }
-    if (tag == 2) { launch_tag<BM, BN, WGM, WGN, 2>(p, st, akc, bkc); return; }
-    if (tag == 3) { launch_tag<BM, BN, WGM, WGN, 3>(p, st, akc, bkc); return; }
-  }
-  launch_tag<BM, BN, WGM, WGN, 0>(p, st, akc, bkc);
+  if (tag == 1) launch_tag<BM, BN, WGM, WGN, 1>(p, st, akc, bkc);
+  else if (tag == 2) launch_tag<BM, BN, WGM, WGN, 2>(p, st, akc, bkc);
+  else if (tag == 3) launch_tag<BM, BN, WGM, WGN, 3>(p, st, akc, bkc);
+  else launch_tag<BM, BN, WGM, WGN, 0>(p, st, akc, bkc);
 }
 
 size_t dgemm_workspace_bytes(const GemmDesc& d) {

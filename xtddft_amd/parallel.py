@@ -1,0 +1,63 @@
+"""Multi-GPU sharding of the TDA operator (one process per GPU).
+
+The reference has no distributed code; the design here
+is SURVEY.md 8(e)'s contraction-dimension sharding:
+
+* rank r keeps aux functions P in ``shard_range(naux, r, n)`` and grid points
+  in ``shard_range(ngrid, r, n)``; everything else (orbitals, Fock, trial
+  vectors, the Davidson subspace) is replicated;
+* every rank evaluates the partial sigma_r of ALL trial vectors from its
+  shard (J, K and XC are sums over P and over grid points, and the MO
+  projections are linear, so sigma = sum_r sigma_r); the one-electron terms
+  are added on rank 0 only;
+* one all-reduce (sum) of sigma per A.x -- ``torch.distributed`` with the
+  ``nccl`` backend, i.e. RCCL over xGMI on MI355X (``gloo`` on CPU in tests).
+
+The Davidson control flow is deterministic given identical inputs, so every
+rank runs it redundantly on the all-reduced sigma and stays in lockstep.
+"""
+from __future__ import annotations
+
+
+def shard_range(n: int, rank: int, nranks: int):
+    """Contiguous [lo, hi) slice of n items for this rank (remainder to low ranks)."""
+    if nranks < 1 or not (0 <= rank < nranks):
+        raise ValueError("bad rank / nranks")
+    base, rem = divmod(n, nranks)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def allreduce_sigma(sigma, group=None):
+    """In-place sum of the per-rank partial sigma (torch tensor)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(sigma, group=group)
+    return sigma
+
+
+class ShardedOperator:
+    """sigma = sum_r A_r z: a rank-local DeviceOperator followed by the all-reduce."""
+
+    def __init__(self, mf, kind, rank=None, nranks=None, device=None, presharded=False, **kw):
+        import torch
+        import torch.distributed as dist
+        from .operator import DeviceOperator
+        if rank is None:
+            rank = dist.get_rank() if dist.is_initialized() else 0
+        if nranks is None:
+            nranks = dist.get_world_size() if dist.is_initialized() else 1
+        if device is None:
+            device = torch.cuda.current_device()
+        self.rank, self.nranks = rank, nranks
+        self.op = DeviceOperator(mf, kind, shard=(rank, nranks), device=device,
+                                 presharded=presharded, **kw)
+        self.dim = self.op.dim
+
+    def apply(self, zs):
+        import torch
+        if not (isinstance(zs, torch.Tensor) and zs.is_cuda):
+            raise TypeError("ShardedOperator works on device tensors")
+        return allreduce_sigma(self.op.apply(zs))
+
+    __call__ = apply
