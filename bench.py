@@ -161,7 +161,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    op.set_profile(0b1110)
+    op.set_profile(0b111110)
     stats_acc = {}
     if world > 1:
         dist.barrier()

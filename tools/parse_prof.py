@@ -16,7 +16,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-TAGS = {1: "df_exchange_contract", 2: "xc_grid_forward", 3: "xc_grid_back"}
+TAGS = {1: "df_exchange_contract", 2: "xc_forward_u", 3: "xc_back_l", 4: "xc_forward_w", 5: "xc_back_m"}
 
 
 def tag_of(name):

@@ -63,6 +63,7 @@ struct xt_ctx {
   bool has_orb = false, has_df = false, has_lr = false, has_grid = false, has_fock = false, has_eps = false;
   DevBuf C, Bmo, Bmo_lr, Phi, kern, F, eps, vects;
   DevBuf ze, acc, kx, zr, tbuf, ubuf, gam, gam2, ws, stage, stage2, zin, sout, trace;
+  DevBuf zp, accT, wbuf;
   hipEvent_t ev[5];
   double timings[4] = {0, 0, 0, 0};
   // live per-kernel timing of tagged GEMM classes (bench roofline); mask bit t = tag t
@@ -70,9 +71,9 @@ struct xt_ctx {
   std::vector<hipEvent_t> pev;     // pairs
   std::vector<int> pev_tag;
   int pev_used = 0;
-  double prof_flops[4] = {0, 0, 0, 0};
-  double prof_ms[4] = {0, 0, 0, 0};
-  int prof_launches[4] = {0, 0, 0, 0};
+  double prof_flops[6] = {0, 0, 0, 0, 0, 0};
+  double prof_ms[6] = {0, 0, 0, 0, 0, 0};
+  int prof_launches[6] = {0, 0, 0, 0, 0, 0};
 };
 
 static int dim_of(const xt_desc& d) {
@@ -94,7 +95,7 @@ static int to_device(xt_ctx* c, DevBuf& dst, const double* src, size_t count, in
 }
 
 static int gemm(xt_ctx* c, const GemmDesc& g) {
-  const bool prof = g.tag > 0 && g.tag < 4 && ((c->prof_mask >> g.tag) & 1);
+  const bool prof = g.tag > 0 && g.tag < 6 && ((c->prof_mask >> g.tag) & 1);
   if (prof) {
     if ((int)c->pev.size() < c->pev_used + 2) {
       hipEvent_t a, b;
@@ -134,7 +135,7 @@ int xt_set_profile(xt_ctx* c, int mask) {
 // device ms, launches and algorithmic flops of GEMM class `tag` in the last
 // xt_apply (one launch = one GEMM call including its split-K reduce)
 int xt_profile_stats(const xt_ctx* c, int tag, double* out3) {
-  if (!c || !out3 || tag < 1 || tag > 3) return fail(XT_ERR_ARG, "bad argument");
+  if (!c || !out3 || tag < 1 || tag > 5) return fail(XT_ERR_ARG, "bad argument");
   out3[0] = c->prof_ms[tag]; out3[1] = c->prof_launches[tag]; out3[2] = c->prof_flops[tag];
   return 0;
 }
@@ -196,7 +197,7 @@ int xt_destroy(xt_ctx* c) {
   (void)hipSetDevice(c->d.device);
   DevBuf* bufs[] = {&c->C, &c->Bmo, &c->Bmo_lr, &c->Phi, &c->kern, &c->F, &c->eps, &c->vects,
                     &c->ze, &c->acc, &c->kx, &c->zr, &c->tbuf, &c->ubuf, &c->gam, &c->gam2, &c->ws,
-                    &c->stage, &c->stage2, &c->zin, &c->sout, &c->trace};
+                    &c->stage, &c->stage2, &c->zin, &c->sout, &c->trace, &c->zp, &c->accT, &c->wbuf};
   for (DevBuf* b : bufs) b->release();
   for (int i = 0; i < 5; ++i) (void)hipEventDestroy(c->ev[i]);
   for (hipEvent_t e : c->pev) (void)hipEventDestroy(e);
@@ -495,46 +496,147 @@ static int left_mo(xt_ctx* c, int nz, int nr, int K, int ncl, const double* F, l
 }
 
 // ---------------------------------------------------------------------------
-// XC response: sigma_ch += sum_c S_c^T PhiV^c  for both spin channels
+// Channel groups.  Spin channels that share one MO basis are contracted
+// together (ROKS X-TDA: both channels form one group of 2*nz "vectors"; UKS:
+// one group per channel; SF/XSF: one channel).  Per group (channels ch0..ch0+nch-1,
+// nzg = nch*nz rows):
+//   Ze   : (nzg, O, V) rows of c->ze starting at channel ch0
+//   Zp   : (O, nzg, V)  permuted copy for contractions over the occupied index
+//   accT : (O, nzg, V)  results of those contractions (exchange, XC back-2),
+//          permute-added into acc at the end of xt_apply
+// ---------------------------------------------------------------------------
+struct Group { int ch0, nch, ob, vb; };
+
+static int channel_groups(const xt_ctx* c, Group* g) {
+  if (c->nchan == 2 && c->occ_basis[0] == c->occ_basis[1] && c->vir_basis[0] == c->vir_basis[1]) {
+    g[0] = {0, 2, c->occ_basis[0], c->vir_basis[0]};
+    return 1;
+  }
+  for (int ch = 0; ch < c->nchan; ++ch) g[ch] = {ch, 1, c->occ_basis[ch], c->vir_basis[ch]};
+  return c->nchan;
+}
+
+// accT_g[(j,x)][b] += coef * sum_P sum_{i,a} B[P][j][i] Zp_g[i][x][a] B[P][v0+a][v0+b]
+static int exchange_main(xt_ctx* c, int nz, const DevBuf& B, double coef) {
+  if (coef == 0.0) return 0;
+  const int O = c->O, V = c->V, nmo = c->d.nmo, naux = c->d.naux;
+  const long mm = (long)nmo * nmo, chs = (long)nz * O * V;
+  Group gr[2];
+  const int ngr = channel_groups(c, gr);
+  for (int q = 0; q < ngr; ++q) {
+    const int nzg = gr[q].nch * nz;
+    const size_t per = (size_t)O * nzg * V;
+    int pc = (int)(((size_t)3 << 30) / (8 * per));
+    if (pc < 1) pc = 1;
+    if (pc > naux) pc = naux;
+    RET(c->tbuf.ensure((size_t)pc * per));
+    const double* Bo = bmo_of(c, B, gr[q].ob);
+    const double* Bv = bmo_of(c, B, gr[q].vb);
+    const double* zp = c->zp.p + gr[q].ch0 * chs;
+    double* at = c->accT.p + gr[q].ch0 * chs;
+    for (int p0 = 0; p0 < naux; p0 += pc) {
+      const int np = (p0 + pc <= naux) ? pc : naux - p0;
+      GemmDesc g1;   // T[P] (O, nzg*V) = B[P][occ][occ] . Zp
+      g1.M = O; g1.N = nzg * V; g1.K = O; g1.nb1 = np;
+      g1.A = Bo + p0 * mm; g1.sAm = nmo; g1.sAk = 1; g1.sAb1 = mm;
+      g1.B = zp; g1.sBk = (long)nzg * V; g1.sBn = 1;
+      g1.C = c->tbuf.p; g1.ldc = (long)nzg * V; g1.sCb1 = (long)per;
+      RET(gemm(c, g1));
+      GemmDesc g2;   // accT[(j,x)][b] += coef * sum_{P,a} T[P][(j,x)][a] B[P][v0+a][v0+b]
+      g2.M = O * nzg; g2.N = V; g2.K = V; g2.R = np;
+      g2.A = c->tbuf.p; g2.sAm = V; g2.sAk = 1; g2.sAr = (long)per;
+      g2.B = Bv + p0 * mm + (long)c->v0 * nmo + c->v0; g2.sBk = nmo; g2.sBn = 1; g2.sBr = mm;
+      g2.C = at; g2.ldc = V;
+      g2.alpha = coef; g2.beta = 1.0;
+      g2.tag = 1;
+      RET(gemm(c, g2));
+    }
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// XC response over the grid (chunks of G points), W route (see k_xc_uks_w):
+//   F1 U = PhiV0 Ze^T ; F2 W = PhiO0 Zp (GGA) ; point kernel ; B1 acc += L^T PhiV0 ;
+//   B2 accT += PhiO0^T M (GGA).  LDA / ALDA0: F1, point kernel, B1.
 // ---------------------------------------------------------------------------
 static int xc_response(xt_ctx* c, int nz) {
   const int O = c->O, V = c->V, nmo = c->d.nmo, ng = c->d.ngrid, nc = c->ncomp;
   const int nch = c->nchan;
+  const bool gga = (nc == 4);
   const long chs = (long)nz * O * V;
-  // grid chunk: U holds nch * ncomp * G * nz*O doubles
-  const size_t per_g = (size_t)nch * nc * nz * O;
-  size_t G = ((size_t)3 << 30) / (8 * per_g);
+  Group gr[2];
+  const int ngr = channel_groups(c, gr);
+  const size_t per_g = (size_t)nch * nz * O + (gga ? (size_t)nch * nz * V : 0);
+  size_t G = ((size_t)4 << 30) / (8 * per_g);
   if (G > (size_t)ng) G = ng;
   if (G < 64) G = 64 < (size_t)ng ? 64 : ng;
-  RET(c->ubuf.ensure(per_g * G));
+  RET(c->ubuf.ensure((size_t)nch * nz * O * G));
+  if (gga) RET(c->wbuf.ensure((size_t)nch * nz * V * G));
   const long compP = (long)ng * nmo;
   const long basP = (long)nc * compP;
   for (int g0 = 0; g0 < ng; g0 += (int)G) {
     const int n = (g0 + (int)G <= ng) ? (int)G : ng - g0;
-    const long ldU = (long)nz * O, compU = (long)n * ldU, chU = (long)nc * compU;
-    for (int ch = 0; ch < nch; ++ch) {
-      GemmDesc g;   // U_c[g][(x,i)] = sum_a PhiV^c[g][a] Ze[x][i][a]
-      g.M = n; g.N = nz * O; g.K = V; g.nb1 = nc;
-      g.A = c->Phi.p + c->vir_basis[ch] * basP + (long)g0 * nmo + c->v0; g.sAm = nmo; g.sAk = 1; g.sAb1 = compP;
-      g.B = c->ze.p + ch * chs; g.sBn = V; g.sBk = 1;
-      g.C = c->ubuf.p + ch * chU; g.ldc = ldU; g.sCb1 = compU;
-      g.tag = 2;
-      RET(gemm(c, g));
+    double* Ug[2]; double* Wg[2]; long ldU[2], ldW[2];
+    for (int q = 0; q < ngr; ++q) {
+      const int nzg = gr[q].nch * nz;
+      Ug[q] = c->ubuf.p + (long)gr[q].ch0 * nz * O * n;  ldU[q] = (long)nzg * O;
+      Wg[q] = gga ? c->wbuf.p + (long)gr[q].ch0 * nz * V * n : nullptr;  ldW[q] = (long)nzg * V;
+      const double* PV = c->Phi.p + gr[q].vb * basP + (long)g0 * nmo + c->v0;
+      const double* PO = c->Phi.p + gr[q].ob * basP + (long)g0 * nmo;
+      GemmDesc f1;   // U[g][(x,i)] = sum_a PhiV0[g][a] Ze[(x,i)][a]
+      f1.M = n; f1.N = nzg * O; f1.K = V;
+      f1.A = PV; f1.sAm = nmo; f1.sAk = 1;
+      f1.B = c->ze.p + gr[q].ch0 * chs; f1.sBn = V; f1.sBk = 1;
+      f1.C = Ug[q]; f1.ldc = ldU[q];
+      f1.tag = 2;
+      RET(gemm(c, f1));
+      if (gga) {
+        GemmDesc f2;   // W[g][(x,a)] = sum_i PhiO0[g][i] Zp[i][(x,a)]
+        f2.M = n; f2.N = nzg * V; f2.K = O;
+        f2.A = PO; f2.sAm = nmo; f2.sAk = 1;
+        f2.B = c->zp.p + gr[q].ch0 * chs; f2.sBk = (long)nzg * V; f2.sBn = 1;
+        f2.C = Wg[q]; f2.ldc = ldW[q];
+        f2.tag = 4;
+        RET(gemm(c, f2));
+      }
     }
     if (nch == 2) {
-      xc_uks(c->st, nc, n, g0, ng, nz, O, nmo, c->Phi.p + c->occ_basis[0] * basP,
-             c->Phi.p + c->occ_basis[1] * basP, c->kern.p, c->ubuf.p);
+      // spin s -> (group, row offset inside the group)
+      double* Us[2]; double* Ws[2]; long lus[2], lws[2];
+      for (int s = 0; s < 2; ++s) {
+        const int q = (ngr == 1) ? 0 : s;
+        const int off = (ngr == 1) ? s : 0;
+        Us[s] = Ug[q] + (long)off * nz * O; lus[s] = ldU[q];
+        Ws[s] = gga ? Wg[q] + (long)off * nz * V : nullptr; lws[s] = ldW[q];
+      }
+      xc_uks_w(c->st, nc, n, g0, ng, nz, O, V, nmo, c->v0, compP,
+               c->Phi.p + c->occ_basis[0] * basP, c->Phi.p + c->occ_basis[1] * basP,
+               c->Phi.p + c->vir_basis[0] * basP, c->Phi.p + c->vir_basis[1] * basP,
+               c->kern.p, Us[0], lus[0], Us[1], lus[1], Ws[0], lws[0], Ws[1], lws[1]);
     } else {
-      xc_sf(c->st, n, g0, nz, O, nmo, c->Phi.p + c->occ_basis[0] * basP, c->kern.p, c->ubuf.p);
+      xc_sf(c->st, n, g0, nz, O, nmo, c->Phi.p + c->occ_basis[0] * basP, c->kern.p, Ug[0]);
     }
-    for (int ch = 0; ch < nch; ++ch) {
-      GemmDesc g;   // acc[(x,i)][a] += sum_{c,g} S_c[g][(x,i)] PhiV^c[g][a]
-      g.M = nz * O; g.N = V; g.K = n; g.R = nc;
-      g.A = c->ubuf.p + ch * chU; g.sAm = 1; g.sAk = ldU; g.sAr = compU;
-      g.B = c->Phi.p + c->vir_basis[ch] * basP + (long)g0 * nmo + c->v0; g.sBk = nmo; g.sBn = 1; g.sBr = compP;
-      g.C = c->acc.p + ch * chs; g.ldc = V; g.beta = 1.0;
-      g.tag = 3;
-      RET(gemm(c, g));
+    for (int q = 0; q < ngr; ++q) {
+      const int nzg = gr[q].nch * nz;
+      const double* PV = c->Phi.p + gr[q].vb * basP + (long)g0 * nmo + c->v0;
+      const double* PO = c->Phi.p + gr[q].ob * basP + (long)g0 * nmo;
+      GemmDesc b1;   // acc[(x,i)][a] += sum_g L[g][(x,i)] PhiV0[g][a]
+      b1.M = nzg * O; b1.N = V; b1.K = n;
+      b1.A = Ug[q]; b1.sAm = 1; b1.sAk = ldU[q];
+      b1.B = PV; b1.sBk = nmo; b1.sBn = 1;
+      b1.C = c->acc.p + gr[q].ch0 * chs; b1.ldc = V; b1.beta = 1.0;
+      b1.tag = 3;
+      RET(gemm(c, b1));
+      if (gga) {
+        GemmDesc b2;   // accT[i][(x,a)] += sum_g PhiO0[g][i] M[g][(x,a)]
+        b2.M = O; b2.N = nzg * V; b2.K = n;
+        b2.A = PO; b2.sAm = 1; b2.sAk = nmo;
+        b2.B = Wg[q]; b2.sBk = ldW[q]; b2.sBn = 1;
+        b2.C = c->accT.p + gr[q].ch0 * chs; b2.ldc = (long)nzg * V; b2.beta = 1.0;
+        b2.tag = 5;
+        RET(gemm(c, b2));
+      }
     }
   }
   return 0;
@@ -657,13 +759,20 @@ extern "C" int xt_apply(xt_ctx* c, int nz, const double* z, double* sigma, int p
   RET(c->ze.ensure(nch * chs));
   RET(c->acc.ensure(nch * chs));
   c->pev_used = 0;
-  for (int t = 0; t < 4; ++t) { c->prof_flops[t] = 0.0; c->prof_ms[t] = 0.0; c->prof_launches[t] = 0; }
+  for (int t = 0; t < 6; ++t) { c->prof_flops[t] = 0.0; c->prof_ms[t] = 0.0; c->prof_launches[t] = 0; }
   HIPCHK(hipEventRecord(c->ev[0], c->st));
   // ---- embed trial vectors -------------------------------------------------
   if (d.kind == XT_KIND_XTDA || d.kind == XT_KIND_UTDA) embed_xtda(c->st, nz, d.nc, d.no, d.nv, zd, c->ze.p);
   else if (xsf) xsf_assemble(c->st, nz, d.nc, d.no, d.nv, d.remove, c->vects.p, zd, c->ze.p);
   else HIPCHK(hipMemcpyAsync(c->ze.p, zd, chs * 8, hipMemcpyDeviceToDevice, c->st));
   HIPCHK(hipMemsetAsync(c->acc.p, 0, nch * chs * 8, c->st));
+  RET(c->zp.ensure(nch * chs));
+  RET(c->accT.ensure(nch * chs));
+  HIPCHK(hipMemsetAsync(c->accT.p, 0, nch * chs * 8, c->st));
+  Group grp[2];
+  const int ngrp = channel_groups(c, grp);
+  for (int q = 0; q < ngrp; ++q)   // Zp_g (O, nzg, V) = permuted Ze_g
+    permute_xi(c->st, grp[q].nch * nz, O, V, c->ze.p + grp[q].ch0 * chs, c->zp.p + grp[q].ch0 * chs);
 
   // ---- one-electron terms (rank-local) --------------------------------------
   if (d.add_local) {
@@ -721,15 +830,8 @@ extern "C" int xt_apply(xt_ctx* c, int nz, const double* z, double* sigma, int p
                             c->acc.p + ch * chs, V, (long)O * V, 1.0));
     }
     if (has_k) {
-      for (int ch = 0; ch < nch; ++ch) {
-        const int ob = c->occ_basis[ch], vb = c->vir_basis[ch];
-        if (c->ck != 0.0)
-          RET(sandwich(c, bmo_of(c, c->Bmo, ob), bmo_of(c, c->Bmo, vb), nz, 0, O, 0, O, c->v0, V, c->v0, V,
-                       c->ze.p + ch * chs, V, (long)O * V, c->acc.p + ch * chs, V, (long)O * V, -c->ck));
-        if (c->ck_lr != 0.0)
-          RET(sandwich(c, bmo_of(c, c->Bmo_lr, ob), bmo_of(c, c->Bmo_lr, vb), nz, 0, O, 0, O, c->v0, V, c->v0, V,
-                       c->ze.p + ch * chs, V, (long)O * V, c->acc.p + ch * chs, V, (long)O * V, -c->ck_lr));
-      }
+      RET(exchange_main(c, nz, c->Bmo, -c->ck));
+      if (c->ck_lr != 0.0) RET(exchange_main(c, nz, c->Bmo_lr, -c->ck_lr));
     }
     if (xsf && d.sa > 0) RET(xsf_delta_a(c, nz));
   }
@@ -737,6 +839,8 @@ extern "C" int xt_apply(xt_ctx* c, int nz, const double* z, double* sigma, int p
 
   // ---- XC ----------------------------------------------------------------------
   if (d.xctype != XT_XC_NONE && d.ngrid > 0) RET(xc_response(c, nz));
+  for (int q = 0; q < ngrp; ++q)   // acc_g += accT_g (left-contraction results)
+    permute_add(c->st, grp[q].nch * nz, O, V, 1.0, c->accT.p + grp[q].ch0 * chs, c->acc.p + grp[q].ch0 * chs);
   HIPCHK(hipEventRecord(c->ev[3], c->st));
 
   // ---- extract -----------------------------------------------------------------

@@ -232,11 +232,23 @@ static void launch_tag(const GemmParams& p, hipStream_t st, bool akc, bool bkc) 
   else             hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, false, false, TAG>), grid, block, 0, st, p);
 }
 
+template <int BM, int BN, int WGM, int WGN, bool AK, bool BKc, int TAG>
+static void launch_one(const GemmParams& p, hipStream_t st) {
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, AK, BKc, TAG>), dim3(tiles, 1, p.nbatch * p.nsplit),
+                     dim3(64 * WGM * WGN), 0, st, p);
+}
+
+// Tagged call sites get their own kernel symbol for their one operand layout:
+// 1 exchange contraction (A k-contig, B n-contig), 2 XC forward U (k, k),
+// 3 XC back L (m, n), 4 XC forward W (k, n), 5 XC back M (m, n).
 template <int BM, int BN, int WGM, int WGN>
 static void launch_cfg(const GemmParams& p, hipStream_t st, bool akc, bool bkc, int tag) {
-  if (tag == 1) launch_tag<BM, BN, WGM, WGN, 1>(p, st, akc, bkc);
-  else if (tag == 2) launch_tag<BM, BN, WGM, WGN, 2>(p, st, akc, bkc);
-  else if (tag == 3) launch_tag<BM, BN, WGM, WGN, 3>(p, st, akc, bkc);
+  if (tag == 1 && akc && !bkc) launch_one<BM, BN, WGM, WGN, true, false, 1>(p, st);
+  else if (tag == 2 && akc && bkc) launch_one<BM, BN, WGM, WGN, true, true, 2>(p, st);
+  else if (tag == 3 && !akc && !bkc) launch_one<BM, BN, WGM, WGN, false, false, 3>(p, st);
+  else if (tag == 4 && akc && !bkc) launch_one<BM, BN, WGM, WGN, true, false, 4>(p, st);
+  else if (tag == 5 && !akc && !bkc) launch_one<BM, BN, WGM, WGN, false, false, 5>(p, st);
   else launch_tag<BM, BN, WGM, WGN, 0>(p, st, akc, bkc);
 }
 

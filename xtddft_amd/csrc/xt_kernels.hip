@@ -262,6 +262,113 @@ k_xc_uks(int G, int g0, int ngrid, int nz, int O, int nmo,
   }
 }
 
+// ---- XC response, "W route" (one 256-thread block per grid point g) ---------
+// Spin channel s of trial vector x holds, at grid point g (g0 + g globally):
+//   U_s[g][x*O + i] = sum_a PhiV0[g][a] Z[x][i][a]      (GEMM, xc forward)
+//   W_s[g][x*V + a] = sum_i PhiO0[g][i] Z[x][i][a]      (GEMM, GGA only)
+// and this kernel forms (PySCF eval_rho for a non-hermitian dm + nr_uks_fxc):
+//   rho1[s][0] = sum_i U PhiO0 ;  rho1[s][c] = sum_i U PhiOc + sum_a W PhiVc
+//   wv[s][y]   = sum_{t,y'} (w fxc)[t,y'][s,y] rho1[t][y']
+//   U <- L = wv0 PhiO0 + sum_c wvc PhiOc ;  W <- M = sum_c wvc PhiVc
+// so that sigma += L^T PhiV0 + PhiO0^T M (two GEMMs, xc back).  The grid point's
+// MO values / gradients are staged once in LDS and reused by all 2*nz vectors.
+template <int NC>
+__global__ void __launch_bounds__(256)
+k_xc_uks_w(int g0, int ngrid, int nz, int O, int V, int nmo, int v0, long compP,
+           const double* __restrict__ pO0, const double* __restrict__ pO1,
+           const double* __restrict__ pV0, const double* __restrict__ pV1,
+           const double* __restrict__ wfxc,
+           double* __restrict__ U0, long ldU0, double* __restrict__ U1, long ldU1,
+           double* __restrict__ W0, long ldW0, double* __restrict__ W1, long ldW1) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int g = blockIdx.x;
+  const long gg = g0 + g;
+  const bool same = (pO0 == pO1);
+  const int per_spin = NC * O + (NC - 1) * V;
+  double* so[2];
+  double* sv[2];
+  so[0] = sm; sv[0] = sm + NC * O;
+  so[1] = same ? so[0] : sm + per_spin; sv[1] = same ? sv[0] : sm + per_spin + NC * O;
+  for (int s = 0; s < (same ? 1 : 2); ++s) {
+    const double* po = s ? pO1 : pO0;
+    const double* pv = s ? pV1 : pV0;
+    for (int k = threadIdx.x; k < NC * O; k += blockDim.x) {
+      const int cc = k / O, i = k % O;
+      so[s][k] = po[cc * compP + gg * nmo + i];
+    }
+    for (int k = threadIdx.x; k < (NC - 1) * V; k += blockDim.x) {
+      const int cc = k / V + 1, a = k % V;
+      sv[s][k] = pv[cc * compP + gg * nmo + v0 + a];
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double* Us[2] = {U0 + g * ldU0, U1 + g * ldU1};
+  double* Ws[2] = {W0 ? W0 + g * ldW0 : nullptr, W1 ? W1 + g * ldW1 : nullptr};
+  for (int x = wave; x < nz; x += 4) {
+    double rho[2][NC];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const double* u = Us[s] + (long)x * O;
+      double acc[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) acc[c] = 0.0;
+      for (int i = lane; i < O; i += 64) {
+        const double uv = u[i];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[c] += uv * so[s][c * O + i];
+      }
+      if (NC > 1) {
+        const double* w = Ws[s] + (long)x * V;
+        for (int a = lane; a < V; a += 64) {
+          const double wa = w[a];
+#pragma unroll
+          for (int c = 1; c < NC; ++c) acc[c] += wa * sv[s][(c - 1) * V + a];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        double v = acc[c];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        rho[s][c] = v;
+      }
+    }
+    double wv[2][NC];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int y = 0; y < NC; ++y) {
+        double v = 0.0;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int yy = 0; yy < NC; ++yy)
+            v += wfxc[((((long)t * NC + yy) * 2 + s) * NC + y) * ngrid + gg] * rho[t][yy];
+        wv[s][y] = v;
+      }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      double* u = Us[s] + (long)x * O;
+      for (int i = lane; i < O; i += 64) {
+        double l = 0.0;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) l += wv[s][c] * so[s][c * O + i];
+        u[i] = l;
+      }
+      if (NC > 1) {
+        double* w = Ws[s] + (long)x * V;
+        for (int a = lane; a < V; a += 64) {
+          double m = 0.0;
+#pragma unroll
+          for (int c = 1; c < NC; ++c) m += wv[s][c] * sv[s][(c - 1) * V + a];
+          w[a] = m;
+        }
+      }
+    }
+  }
+}
+
 // ALDA0 spin-flip kernel (SF_TDA.py:90-160): rho1 = sum_i U0 PhiO, wv = rho1*fsf, S0 = wv*PhiO
 __global__ void __launch_bounds__(256)
 k_xc_sf(int G, int g0, int nz, int O, int nmo, const double* __restrict__ phio,
@@ -439,6 +546,20 @@ void xc_uks(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, 
     hipLaunchKernelGGL(k_xc_uks<4>, dim3(blocks), dim3(256), 0, st, G, g0, ngrid, nz, O, nmo, phi0, phi1, wfxc, U);
   else
     hipLaunchKernelGGL(k_xc_uks<1>, dim3(blocks), dim3(256), 0, st, G, g0, ngrid, nz, O, nmo, phi0, phi1, wfxc, U);
+}
+void xc_uks_w(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, int V, int nmo, int v0,
+              long compP, const double* pO0, const double* pO1, const double* pV0, const double* pV1,
+              const double* wfxc, double* U0, long ldU0, double* U1, long ldU1,
+              double* W0, long ldW0, double* W1, long ldW1) {
+  const bool same = (pO0 == pO1);
+  const size_t per_spin = (size_t)ncomp * O + (size_t)(ncomp - 1) * V;
+  const size_t lds = (same ? 1 : 2) * per_spin * sizeof(double);
+  if (ncomp == 4)
+    hipLaunchKernelGGL(k_xc_uks_w<4>, dim3(G), dim3(256), lds, st, g0, ngrid, nz, O, V, nmo, v0, compP,
+                       pO0, pO1, pV0, pV1, wfxc, U0, ldU0, U1, ldU1, W0, ldW0, W1, ldW1);
+  else
+    hipLaunchKernelGGL(k_xc_uks_w<1>, dim3(G), dim3(256), lds, st, g0, ngrid, nz, O, V, nmo, v0, compP,
+                       pO0, pO1, pV0, pV1, wfxc, U0, ldU0, U1, ldU1, W0, ldW0, W1, ldW1);
 }
 void xc_sf(hipStream_t st, int G, int g0, int nz, int O, int nmo, const double* phio, const double* fsf, double* U) {
   const long waves = (long)G * nz;

@@ -185,10 +185,11 @@ class DeviceOperator:
         _capi.check(self._L.xt_last_timings(self._h, ctypes.cast(buf, ctypes.c_void_p)), "timings")
         return dict(jk_ms=buf[0], xc_ms=buf[1], local_ms=buf[2], total_ms=buf[3])
 
-    PROFILE_TAGS = {1: "df_exchange_contract", 2: "xc_grid_forward", 3: "xc_grid_back"}
+    PROFILE_TAGS = {1: "df_exchange_contract", 2: "xc_forward_u", 3: "xc_back_l",
+                    4: "xc_forward_w", 5: "xc_back_m"}
 
-    def set_profile(self, mask: int = 0b1110):
-        """Time GEMM classes live with HIP events (bit 1 exchange, 2 XC forward, 3 XC back)."""
+    def set_profile(self, mask: int = 0b111110):
+        """Time GEMM classes live with HIP events (bit t = tag t, see PROFILE_TAGS)."""
         _capi.check(self._L.xt_set_profile(self._h, int(mask)), "xt_set_profile")
 
     def profile_stats(self):
