@@ -13,14 +13,14 @@
 // second level of a two-level contraction (e.g. P in sum_P sum_b), so no
 // operand is ever re-laid-out in HBM to fit a plain GEMM.
 //
-// Tiling: BM x BN block tile, BK = 16, WGM x WGN waves (128x128: 2x4 waves,
+// Tiling: BM x BN block tile, BK = 32, WGM x WGN waves (128x128: 2x4 waves,
 // 512 threads; smaller tiles 2x2), each wave (BM/WGM)x(BN/WGN) made of 16x16
 // v_mfma_f64_16x16x4_f64 tiles.
-// LDS holds As[m][k] / Bs[n][k] (k contiguous, row pitch 18 doubles), double
-// buffered with register staging.  Lane l (q = l>>4) feeds MFMA step s of a
-// K-tile with k = 4q + s, so each lane reads 4 consecutive k per operand
-// (one 8-byte LDS read per MFMA step) -- the k permutation is applied
-// identically to A and B, so the sum over k is unchanged.
+// LDS holds As[m][k] / Bs[n][k] (k contiguous, odd row pitch 33 doubles),
+// double buffered with register staging.  Lane l (q = l>>4) feeds MFMA step s
+// of a K-tile with k = q + 4s -- the k permutation is applied identically to
+// A and B, so the sum over k is unchanged.  Staging addresses are per-thread
+// 32-bit offsets computed once; the K loop body is branch-free.
 // C/D layout of the f64 MFMA: col = lane & 15, row = (lane >> 4) + 4*reg
 // (checked on hardware, tools/mfma_probe.hip).
 //
@@ -37,11 +37,16 @@ namespace xt {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-constexpr int BK = 16;
-constexpr int LDP = 18;          // LDS row pitch in doubles (16 + 2 pad, keeps 16-B alignment)
+constexpr int BK = 32;
+// LDS row pitch in doubles.  The compiler pairs the per-step fragment reads into
+// ds_read2_b64, whose lane groups are 16 lanes over 32 banks: lane (q, r) of a
+// group reads row r at k = q + 4s, i.e. dword 2*(LDP*r + q) mod 32, which is
+// conflict-free for any odd pitch.  Odd pitch also keeps both staging stores
+// (16 consecutive k of one row, or one k of 16 consecutive rows) conflict-free.
+constexpr int LDP = BK + 1;
+constexpr int GROUP_M = 8;       // m-tiles per grouped sweep over n (L2 panel reuse)
 
-// TAG only gives hot call sites their own kernel symbol (rocprofv3 identity):
-// 1 = DF-exchange contraction, 2 = XC grid forward, 3 = XC grid back-projection.
+// TAG only gives hot call sites their own kernel symbol (rocprofv3 identity).
 template <int BM, int BN, int WGM, int WGN, bool A_KC, bool B_KC, int TAG>
 __global__ void __launch_bounds__(64 * WGM * WGN, 2)
 dgemm_kernel(GemmParams p) {
@@ -51,6 +56,11 @@ dgemm_kernel(GemmParams p) {
   constexpr int A_ELEMS = BM * BK / NTHREADS;    // doubles staged per thread
   constexpr int B_ELEMS = BN * BK / NTHREADS;
   constexpr int STAGE = (BM + BN) * LDP;         // one LDS buffer (A then B)
+  // staging geometry: a K-contiguous operand is staged as k = tid % BK of rows
+  // tid / BK + e * STEP; an MN-contiguous one as m = tid % BM of k-rows tid / BM + e * STEP
+  constexpr int A_STEP = A_KC ? NTHREADS / BK : NTHREADS / BM;
+  constexpr int B_STEP = B_KC ? NTHREADS / BK : NTHREADS / BN;
+  static_assert(NTHREADS % BK == 0 && NTHREADS % BM == 0 && NTHREADS % BN == 0, "staging map");
 
   __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
 
@@ -61,14 +71,26 @@ dgemm_kernel(GemmParams p) {
   const int q = lane >> 4, r16 = lane & 15;
 
   // ---- block -> (tile, batch, split) ---------------------------------------
+  // Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
+  // "Workgroup dispatch"); renumber so each XCD runs a contiguous range of
+  // tiles, and walk tiles in GROUP_M-tall column sweeps so the blocks resident
+  // on one XCD share A and B panels in its L2.
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.N + BN - 1) / BN;
-  int tile = blockIdx.x;
-  // group consecutive blocks along m so blocks sharing a B panel run together
-  const int tm = tile % tiles_m;
-  const int tn = tile / tiles_m;
-  if (tn >= tiles_n) return;
-  const int z = blockIdx.z;
+  const int ntile = tiles_m * tiles_n;
+  int lid = blockIdx.x + ntile * blockIdx.z;
+  {
+    const int nblk = ntile * gridDim.z;
+    const int xcd = lid & 7, idx = lid >> 3, qn = nblk >> 3, rem = nblk & 7;
+    lid = xcd * qn + (xcd < rem ? xcd : rem) + idx;
+  }
+  const int z = lid / ntile;
+  const int tile = lid - z * ntile;
+  const int per_group = GROUP_M * tiles_n;
+  const int first_m = (tile / per_group) * GROUP_M;
+  const int gsz = (tiles_m - first_m < GROUP_M) ? tiles_m - first_m : GROUP_M;
+  const int tm = first_m + (tile % per_group) % gsz;
+  const int tn = (tile % per_group) / gsz;
   const int split = z % p.nsplit;
   const int b = z / p.nsplit;
   const int b1 = b / p.nb2, b2 = b % p.nb2;
@@ -80,8 +102,10 @@ dgemm_kernel(GemmParams p) {
   const long u0 = split * u_per;
   const long u1 = (u0 + u_per < units) ? (u0 + u_per) : units;
 
-  const double* __restrict__ Ab = p.A + b1 * p.sAb1 + b2 * p.sAb2;
-  const double* __restrict__ Bb = p.B + b1 * p.sBb1 + b2 * p.sBb2;
+  const double* __restrict__ Ab = p.A + b1 * p.sAb1 + b2 * p.sAb2 +
+                                  (A_KC ? (long)m0 * p.sAm : (long)m0);
+  const double* __restrict__ Bb = p.B + b1 * p.sBb1 + b2 * p.sBb2 +
+                                  (B_KC ? (long)n0 * p.sBn : (long)n0);
 
   d4 acc[TM][TN];
 #pragma unroll
@@ -89,83 +113,123 @@ dgemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
 
+  // Per-thread byte offsets from the tile origin, fixed for the whole K loop.
+  // Rows (cols) past M (N) are clamped to the last valid one: they only feed
+  // accumulator rows (cols) that are never stored.  32-bit offsets: dgemm()
+  // rejects strides that would overflow them.
+  const int a_fix = A_KC ? tid % BK : tid % BM, a_var = A_KC ? tid / BK : tid / BM;
+  const int b_fix = B_KC ? tid % BK : tid % BN, b_var = B_KC ? tid / BK : tid / BN;
+  unsigned aoff[A_ELEMS], boff[B_ELEMS];
+  unsigned a_row0, b_row0;   // MN-contiguous operands: offset of k-row 0 (k-edge fallback)
+#pragma unroll
+  for (int e = 0; e < A_ELEMS; ++e) {
+    if (A_KC) {
+      int mm = min(m0 + a_var + e * A_STEP, p.M - 1) - m0;
+      aoff[e] = (unsigned)(((long)mm * p.sAm + a_fix) * 8);
+    } else {
+      int mm = min(m0 + a_fix, p.M - 1) - m0;
+      aoff[e] = (unsigned)(((long)(a_var + e * A_STEP) * p.sAk + mm) * 8);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < B_ELEMS; ++e) {
+    if (B_KC) {
+      int nn = min(n0 + b_var + e * B_STEP, p.N - 1) - n0;
+      boff[e] = (unsigned)(((long)nn * p.sBn + b_fix) * 8);
+    } else {
+      int nn = min(n0 + b_fix, p.N - 1) - n0;
+      boff[e] = (unsigned)(((long)(b_var + e * B_STEP) * p.sBk + nn) * 8);
+    }
+  }
+  a_row0 = (unsigned)((min(m0 + a_fix, p.M - 1) - m0) * 8);
+  b_row0 = (unsigned)((min(n0 + b_fix, p.N - 1) - n0) * 8);
+
   double ra[A_ELEMS], rb[B_ELEMS];
 
-  // staging index maps.  K-contiguous: 16 threads cover one row's 16 k.
-  // MN-contiguous: consecutive threads cover consecutive m (or n) of one k.
-  auto load_tile = [&](long u) {
-    const int r = (int)(u / nkt);
-    const int k0 = (int)(u % nkt) * BK;
-    const double* Ar = Ab + (long)r * p.sAr;
-    const double* Br = Bb + (long)r * p.sBr;
+  // Stage K-tile (r, kt) into registers.  Branch-free: k past K (last tile of
+  // each r) reads k = 0 of the same row instead; the B copy of those k is
+  // zeroed in store_tile, so they add nothing.  Returns the valid k count.
+  auto load_tile = [&](int r, int kt) -> int {
+    const int k0 = kt * BK;
+    const int kv = p.K - k0;
+    const char* At = (const char*)(Ab + (long)r * p.sAr + (A_KC ? (long)k0 : (long)k0 * p.sAk));
+    const char* Bt = (const char*)(Bb + (long)r * p.sBr + (B_KC ? (long)k0 : (long)k0 * p.sBk));
 #pragma unroll
     for (int e = 0; e < A_ELEMS; ++e) {
-      int idx = tid + e * NTHREADS;
-      int mm, kk;
-      if (A_KC) { mm = idx / BK; kk = idx % BK; } else { kk = idx / BM; mm = idx % BM; }
-      int gm = m0 + mm, gk = k0 + kk;
-      double v = 0.0;
-      if (gm < p.M && gk < p.K)
-        v = A_KC ? Ar[(long)gm * p.sAm + gk] : Ar[(long)gk * p.sAk + gm];
-      ra[e] = v;
+      unsigned o;
+      if (A_KC) o = (a_fix < kv) ? aoff[e] : aoff[e] - (unsigned)(a_fix * 8);
+      else      o = (a_var + e * A_STEP < kv) ? aoff[e] : a_row0;
+      ra[e] = *(const double*)(At + o);
     }
 #pragma unroll
     for (int e = 0; e < B_ELEMS; ++e) {
-      int idx = tid + e * NTHREADS;
-      int nn, kk;
-      if (B_KC) { nn = idx / BK; kk = idx % BK; } else { kk = idx / BN; nn = idx % BN; }
-      int gn = n0 + nn, gk = k0 + kk;
-      double v = 0.0;
-      if (gn < p.N && gk < p.K)
-        v = B_KC ? Br[(long)gn * p.sBn + gk] : Br[(long)gk * p.sBk + gn];
-      rb[e] = v;
+      unsigned o;
+      if (B_KC) o = (b_fix < kv) ? boff[e] : boff[e] - (unsigned)(b_fix * 8);
+      else      o = (b_var + e * B_STEP < kv) ? boff[e] : b_row0;
+      rb[e] = *(const double*)(Bt + o);
     }
+    return kv;
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, int kv) {
 #pragma unroll
     for (int e = 0; e < A_ELEMS; ++e) {
-      int idx = tid + e * NTHREADS;
       int mm, kk;
-      if (A_KC) { mm = idx / BK; kk = idx % BK; } else { kk = idx / BM; mm = idx % BM; }
+      if (A_KC) { mm = a_var + e * A_STEP; kk = a_fix; } else { kk = a_var + e * A_STEP; mm = a_fix; }
       smem[buf * STAGE + mm * LDP + kk] = ra[e];
     }
 #pragma unroll
     for (int e = 0; e < B_ELEMS; ++e) {
-      int idx = tid + e * NTHREADS;
       int nn, kk;
-      if (B_KC) { nn = idx / BK; kk = idx % BK; } else { kk = idx / BN; nn = idx % BN; }
-      smem[buf * STAGE + BM * LDP + nn * LDP + kk] = rb[e];
+      if (B_KC) { nn = b_var + e * B_STEP; kk = b_fix; } else { kk = b_var + e * B_STEP; nn = b_fix; }
+      smem[buf * STAGE + BM * LDP + nn * LDP + kk] = (kk < kv) ? rb[e] : 0.0;
     }
   };
   auto compute = [&](int buf) {
-    const int abase = buf * STAGE + (wm * WM + r16) * LDP + 4 * q;
-    const int bbase = buf * STAGE + BM * LDP + (wn * WN + r16) * LDP + 4 * q;
+    const int abase = buf * STAGE + (wm * WM + r16) * LDP + q;
+    const int bbase = buf * STAGE + BM * LDP + (wn * WN + r16) * LDP + q;
+    constexpr int SK = BK / 4;   // MFMA k-steps per tile
+    double af[2][TM], bf[2][TN];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      double af[TM], bf[TN];
+    for (int i = 0; i < TM; ++i) af[0][i] = smem[abase + i * 16 * LDP];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = smem[abase + i * 16 * LDP + s];
+    for (int j = 0; j < TN; ++j) bf[0][j] = smem[bbase + j * 16 * LDP];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = smem[bbase + j * 16 * LDP + s];
+    for (int s = 0; s < SK; ++s) {
+      const int cur = s & 1, nxt = cur ^ 1;
+      if (s + 1 < SK) {   // prefetch the next step's fragments behind this step's MFMAs
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[nxt][i] = smem[abase + i * 16 * LDP + 4 * (s + 1)];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bf[nxt][j] = smem[bbase + j * 16 * LDP + 4 * (s + 1)];
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[cur][i], bf[cur][j], acc[i][j], 0, 0, 0);
     }
   };
 
   if (u0 < u1) {
-    load_tile(u0);
-    store_tile(0);
+    int r = (int)(u0 / nkt), kt = (int)(u0 % nkt);
+    int kv = load_tile(r, kt);
+    store_tile(0, kv);
     __syncthreads();
     int buf = 0;
     for (long u = u0; u < u1; ++u) {
-      const bool more = (u + 1 < u1);
-      if (more) load_tile(u + 1);
+      // next tile; the last pass re-stages its own tile into the idle buffer
+      // (harmless) so the loop body has no branches around the loads
+      int ktn = kt + 1, rn = r;
+      if (ktn == nkt) { ktn = 0; rn = r + 1; }
+      if (u + 1 >= u1) { ktn = kt; rn = r; }
+      kv = load_tile(rn, ktn);
       compute(buf);
-      if (more) store_tile(buf ^ 1);
+      // keep the LDS stores (and their vmcnt waits) behind every MFMA of this
+      // tile: hoisted into the MFMA stream they stall it on global latency
+      __builtin_amdgcn_sched_barrier(0);
+      store_tile(buf ^ 1, kv);
       __syncthreads();
+      r = rn; kt = ktn;
       buf ^= 1;
     }
   }
@@ -296,6 +360,10 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
   const bool bkc = (d.sBk == 1);
   if (!akc && d.sAm != 1) return XT_ERR_ARG;
   if (!bkc && d.sBn != 1) return XT_ERR_ARG;
+  // the kernel addresses a tile with 32-bit byte offsets from its origin
+  const long lim = 1L << 32;
+  if ((akc ? (128L * d.sAm + BK) : (BK * d.sAk + 128L)) * 8 >= lim) return XT_ERR_ARG;
+  if ((bkc ? (128L * d.sBn + BK) : (BK * d.sBk + 128L)) * 8 >= lim) return XT_ERR_ARG;
   GemmParams p; int bm, bn;
   plan_gemm(d, &p, &bm, &bn);
   if (d.K <= 0) {   // C = beta*C
