@@ -31,6 +31,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include "xt_internal.h"
 
 namespace xt {
@@ -67,7 +68,8 @@ dgemm_kernel(GemmParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave / WGN, wn = wave % WGN;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);   // wave-uniform (SGPR) copy
+  const int wm = wave_u / WGN, wn = wave_u % WGN;
   const int q = lane >> 4, r16 = lane & 15;
 
   // ---- block -> (tile, batch, split) ---------------------------------------
@@ -184,10 +186,24 @@ dgemm_kernel(GemmParams p) {
       smem[buf * STAGE + BM * LDP + nn * LDP + kk] = (kk < kv) ? rb[e] : 0.0;
     }
   };
-  auto compute = [&](int buf) {
+  // MFMA sub-tiles of this wave that hold any row < M / col < N; a wave whose
+  // sub-tiles are all in range on a K-full tile takes the pipelined path
+  int mi = (p.M - m0 - wm * WM + 15) / 16;
+  int nj = (p.N - n0 - wn * WN + 15) / 16;
+  mi = mi < 0 ? 0 : (mi > TM ? TM : mi);
+  nj = nj < 0 ? 0 : (nj > TN ? TN : nj);
+  const bool wave_full = (mi == TM) && (nj == TN);
+  constexpr int SK = BK / 4;   // MFMA k-steps per tile
+  // One K-tile of MFMAs, fragments software-pipelined one k-step ahead.
+  // MN_EDGE: skip MFMAs of sub-tiles wholly past M / N (their accumulators are
+  // never stored); K_EDGE: skip k-steps wholly past K (their B rows are zero).
+  // Fragment reads stay unconditional (LDS holds clamped rows), so the read
+  // pipelining is identical in every variant.
+  auto compute = [&](int buf, auto MN_EDGE, auto K_EDGE, int kv) {
+    constexpr bool mn_edge = decltype(MN_EDGE)::value;
+    constexpr bool k_edge = decltype(K_EDGE)::value;
     const int abase = buf * STAGE + (wm * WM + r16) * LDP + q;
     const int bbase = buf * STAGE + BM * LDP + (wn * WN + r16) * LDP + q;
-    constexpr int SK = BK / 4;   // MFMA k-steps per tile
     double af[2][TM], bf[2][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i) af[0][i] = smem[abase + i * 16 * LDP];
@@ -206,24 +222,28 @@ dgemm_kernel(GemmParams p) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[cur][i], bf[cur][j], acc[i][j], 0, 0, 0);
+          if ((!k_edge || 4 * s < kv) && (!mn_edge || (i < mi && j < nj)))
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[cur][i], bf[cur][j], acc[i][j], 0, 0, 0);
     }
   };
 
-  if (u0 < u1) {
+  // The K loop.  All tiles but the last run the branch-free pipelined body
+  // (loads of tile u+1 interleave with the MFMAs of tile u); the last tile,
+  // which is the K-edge tile whenever K % BK != 0 and R == 1, is peeled and
+  // skips the k-steps past K.  Waves whose sub-tiles reach past M / N run the
+  // MN_EDGE variant of the same loop (wave-uniform choice; both variants pass
+  // the same barriers).
+  auto run = [&](auto MN_EDGE) {
     int r = (int)(u0 / nkt), kt = (int)(u0 % nkt);
     int kv = load_tile(r, kt);
     store_tile(0, kv);
     __syncthreads();
     int buf = 0;
-    for (long u = u0; u < u1; ++u) {
-      // next tile; the last pass re-stages its own tile into the idle buffer
-      // (harmless) so the loop body has no branches around the loads
+    for (long u = u0; u + 1 < u1; ++u) {
       int ktn = kt + 1, rn = r;
       if (ktn == nkt) { ktn = 0; rn = r + 1; }
-      if (u + 1 >= u1) { ktn = kt; rn = r; }
       kv = load_tile(rn, ktn);
-      compute(buf);
+      compute(buf, MN_EDGE, std::false_type{}, BK);
       // keep the LDS stores (and their vmcnt waits) behind every MFMA of this
       // tile: hoisted into the MFMA stream they stall it on global latency
       __builtin_amdgcn_sched_barrier(0);
@@ -232,6 +252,11 @@ dgemm_kernel(GemmParams p) {
       r = rn; kt = ktn;
       buf ^= 1;
     }
+    compute(buf, MN_EDGE, std::true_type{}, p.K - kt * BK);
+  };
+  if (u0 < u1) {
+    if (wave_full) run(std::false_type{});
+    else           run(std::true_type{});
   }
 
   // ---- epilogue ------------------------------------------------------------

@@ -271,9 +271,13 @@ k_xc_uks(int G, int g0, int ngrid, int nz, int O, int nmo,
 //   wv[s][y]   = sum_{t,y'} (w fxc)[t,y'][s,y] rho1[t][y']
 //   U <- L = wv0 PhiO0 + sum_c wvc PhiOc ;  W <- M = sum_c wvc PhiVc
 // so that sigma += L^T PhiV0 + PhiO0^T M (two GEMMs, xc back).  The grid point's
-// MO values / gradients are staged once in LDS and reused by all 2*nz vectors.
+// MO values / gradients and the 2NC x 2NC kernel block are staged once in LDS
+// and reused by all 2*nz vectors.  The kernel streams U/W in and L/M out
+// (HBM-bound): each wave handles one x for both spins and keeps
+// 2 x XW_UNR independent 8-byte loads per lane in flight over the W rows.
+constexpr int XW_UNR = 8;
 template <int NC>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 4)
 k_xc_uks_w(int g0, int ngrid, int nz, int O, int V, int nmo, int v0, long compP,
            const double* __restrict__ pO0, const double* __restrict__ pO1,
            const double* __restrict__ pV0, const double* __restrict__ pV1,
@@ -281,60 +285,88 @@ k_xc_uks_w(int g0, int ngrid, int nz, int O, int V, int nmo, int v0, long compP,
            double* __restrict__ U0, long ldU0, double* __restrict__ U1, long ldU1,
            double* __restrict__ W0, long ldW0, double* __restrict__ W1, long ldW1) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
+  __shared__ double sk[4 * NC * NC];   // sk[((t*NC + y')*2 + s)*NC + y] = (w fxc) at this point
   const int g = blockIdx.x;
   const long gg = g0 + g;
   const bool same = (pO0 == pO1);
   const int per_spin = NC * O + (NC - 1) * V;
-  double* so[2];
-  double* sv[2];
+  const double* so[2];
+  const double* sv[2];
   so[0] = sm; sv[0] = sm + NC * O;
   so[1] = same ? so[0] : sm + per_spin; sv[1] = same ? sv[0] : sm + per_spin + NC * O;
   for (int s = 0; s < (same ? 1 : 2); ++s) {
     const double* po = s ? pO1 : pO0;
     const double* pv = s ? pV1 : pV0;
+    double* dso = sm + s * per_spin;
+    double* dsv = dso + NC * O;
     for (int k = threadIdx.x; k < NC * O; k += blockDim.x) {
       const int cc = k / O, i = k % O;
-      so[s][k] = po[cc * compP + gg * nmo + i];
+      dso[k] = po[cc * compP + gg * nmo + i];
     }
     for (int k = threadIdx.x; k < (NC - 1) * V; k += blockDim.x) {
       const int cc = k / V + 1, a = k % V;
-      sv[s][k] = pv[cc * compP + gg * nmo + v0 + a];
+      dsv[k] = pv[cc * compP + gg * nmo + v0 + a];
     }
   }
+  for (int k = threadIdx.x; k < 4 * NC * NC; k += blockDim.x) sk[k] = wfxc[(long)k * ngrid + gg];
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  double* Us[2] = {U0 + g * ldU0, U1 + g * ldU1};
-  double* Ws[2] = {W0 ? W0 + g * ldW0 : nullptr, W1 ? W1 + g * ldW1 : nullptr};
-  for (int x = wave; x < nz; x += 4) {
-    double rho[2][NC];
+  const int nwave = blockDim.x >> 6;
+  double* Ub[2] = {U0 + g * ldU0, U1 + g * ldU1};
+  double* Wb[2] = {W0 ? W0 + g * ldW0 : nullptr, W1 ? W1 + g * ldW1 : nullptr};
+  for (int x = wave; x < nz; x += nwave) {
+    double acc[2][NC];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const double* u = Us[s] + (long)x * O;
-      double acc[NC];
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int c = 0; c < NC; ++c) acc[c] = 0.0;
-      for (int i = lane; i < O; i += 64) {
-        const double uv = u[i];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) acc[c] += uv * so[s][c * O + i];
-      }
-      if (NC > 1) {
-        const double* w = Ws[s] + (long)x * V;
-        for (int a = lane; a < V; a += 64) {
-          const double wa = w[a];
-#pragma unroll
-          for (int c = 1; c < NC; ++c) acc[c] += wa * sv[s][(c - 1) * V + a];
-        }
-      }
+      for (int c = 0; c < NC; ++c) acc[s][c] = 0.0;
+    const double* u0 = Ub[0] + (long)x * O;
+    const double* u1 = Ub[1] + (long)x * O;
+    for (int i = lane; i < O; i += 64) {
+      const double a0 = u0[i], a1 = u1[i];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        double v = acc[c];
+        acc[0][c] += a0 * so[0][c * O + i];
+        acc[1][c] += a1 * so[1][c * O + i];
+      }
+    }
+    if (NC > 1) {
+      const double* w0 = Wb[0] + (long)x * V;
+      const double* w1 = Wb[1] + (long)x * V;
+      for (int a0 = lane; a0 < V; a0 += 64 * XW_UNR) {
+        double r0[XW_UNR], r1[XW_UNR];
+#pragma unroll
+        for (int u = 0; u < XW_UNR; ++u) {   // unconditional (clamped) loads: all in flight at once
+          const int a = min(a0 + 64 * u, V - 1);
+          r0[u] = w0[a];
+          r1[u] = w1[a];
+        }
+#pragma unroll
+        for (int u = 0; u < XW_UNR; ++u) {
+          const int a = min(a0 + 64 * u, V - 1);
+          if (a0 + 64 * u >= V) { r0[u] = 0.0; r1[u] = 0.0; }
+#pragma unroll
+          for (int c = 1; c < NC; ++c) {
+            acc[0][c] += r0[u] * sv[0][(c - 1) * V + a];
+            acc[1][c] += r1[u] * sv[1][(c - 1) * V + a];
+          }
+        }
+      }
+    }
+    double rho[2][NC];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        double v = acc[s][c];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         rho[s][c] = v;
       }
-    }
     double wv[2][NC];
+    // keep the 4 NC^2 kernel values in LDS (re-read per x): hoisted out of the
+    // x loop they would pin 2*4 NC^2 VGPRs
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -343,13 +375,12 @@ k_xc_uks_w(int g0, int ngrid, int nz, int O, int V, int nmo, int v0, long compP,
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int yy = 0; yy < NC; ++yy)
-            v += wfxc[((((long)t * NC + yy) * 2 + s) * NC + y) * ngrid + gg] * rho[t][yy];
+          for (int yy = 0; yy < NC; ++yy) v += sk[((t * NC + yy) * 2 + s) * NC + y] * rho[t][yy];
         wv[s][y] = v;
       }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      double* u = Us[s] + (long)x * O;
+      double* u = Ub[s] + (long)x * O;
       for (int i = lane; i < O; i += 64) {
         double l = 0.0;
 #pragma unroll
@@ -357,7 +388,7 @@ k_xc_uks_w(int g0, int ngrid, int nz, int O, int V, int nmo, int v0, long compP,
         u[i] = l;
       }
       if (NC > 1) {
-        double* w = Ws[s] + (long)x * V;
+        double* w = Wb[s] + (long)x * V;
         for (int a = lane; a < V; a += 64) {
           double m = 0.0;
 #pragma unroll
