@@ -13,10 +13,9 @@
 // second level of a two-level contraction (e.g. P in sum_P sum_b), so no
 // operand is ever re-laid-out in HBM to fit a plain GEMM.
 //
-// Tiling: BM x BN block tile, BK = 32, WGM x WGN waves (128x128: 2x4 waves,
-// 512 threads; smaller tiles 2x2), each wave (BM/WGM)x(BN/WGN) made of 16x16
-// v_mfma_f64_16x16x4_f64 tiles.
-// LDS holds As[m][k] / Bs[n][k] (k contiguous, odd row pitch 33 doubles),
+// Tiling: BM x BN block tile, BK-deep K tiles, WGM x WGN waves, each wave
+// (BM/WGM)x(BN/WGN) made of 16x16 v_mfma_f64_16x16x4_f64 tiles (configs: kCfg).
+// LDS holds As[m][k] / Bs[n][k] (k contiguous, odd row pitch BK + 1 doubles),
 // double buffered with register staging.  Lane l (q = l>>4) feeds MFMA step s
 // of a K-tile with k = q + 4s -- the k permutation is applied identically to
 // A and B, so the sum over k is unchanged.  Staging addresses are per-thread
@@ -32,25 +31,31 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
+#include <stdlib.h>
+#include <map>
+#include <mutex>
+#include <queue>
+#include <tuple>
+#include <vector>
 #include "xt_internal.h"
 
 namespace xt {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-constexpr int BK = 32;
-// LDS row pitch in doubles.  The compiler pairs the per-step fragment reads into
+// LDS row pitch in doubles (LDP = BK + 1).  The compiler pairs the per-step fragment reads into
 // ds_read2_b64, whose lane groups are 16 lanes over 32 banks: lane (q, r) of a
 // group reads row r at k = q + 4s, i.e. dword 2*(LDP*r + q) mod 32, which is
 // conflict-free for any odd pitch.  Odd pitch also keeps both staging stores
 // (16 consecutive k of one row, or one k of 16 consecutive rows) conflict-free.
-constexpr int LDP = BK + 1;
 constexpr int GROUP_M = 8;       // m-tiles per grouped sweep over n (L2 panel reuse)
 
 // TAG only gives hot call sites their own kernel symbol (rocprofv3 identity).
-template <int BM, int BN, int WGM, int WGN, bool A_KC, bool B_KC, int TAG>
-__global__ void __launch_bounds__(64 * WGM * WGN, 2)
+// MINW = waves per SIMD the register budget must allow (occupancy target).
+template <int BM, int BN, int WGM, int WGN, int BK, int MINW, bool A_KC, bool B_KC, int TAG>
+__global__ void __launch_bounds__(64 * WGM * WGN, MINW)
 dgemm_kernel(GemmParams p) {
+  constexpr int LDP = BK + 1;
   constexpr int NTHREADS = 64 * WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;    // wave tile
   constexpr int TM = WM / 16, TN = WN / 16;      // MFMA tiles per wave
@@ -246,6 +251,7 @@ dgemm_kernel(GemmParams p) {
       compute(buf, MN_EDGE, std::false_type{}, BK);
       // keep the LDS stores (and their vmcnt waits) behind every MFMA of this
       // tile: hoisted into the MFMA stream they stall it on global latency
+      // (measured: stores pinned mid-tile are 3-5 % slower)
       __builtin_amdgcn_sched_barrier(0);
       store_tile(buf ^ 1, kv);
       __syncthreads();
@@ -310,46 +316,129 @@ __global__ void splitk_reduce(GemmParams p) {
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int TAG>
-static void launch_tag(const GemmParams& p, hipStream_t st, bool akc, bool bkc) {
-  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  dim3 grid(tiles, 1, p.nbatch * p.nsplit);
-  dim3 block(64 * WGM * WGN);
-  if (akc && bkc)  hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, true, true, TAG>), grid, block, 0, st, p);
-  else if (akc)    hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, true, false, TAG>), grid, block, 0, st, p);
-  else if (bkc)    hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, false, true, TAG>), grid, block, 0, st, p);
-  else             hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, false, false, TAG>), grid, block, 0, st, p);
-}
+// Tile configurations.  C8: 128x128, 8 waves (64x32 each), BK 32, one block
+// per CU (135 KB LDS).  C4: 128x128, 4 waves (64x64 each), BK 16, two blocks
+// per CU (70 KB LDS each) so one block's barrier / prologue / epilogue hides
+// under the other's MFMAs.  Narrow tiles for small M or N.
+struct Cfg { int bm, bn, bk, slots, wgm, wgn; };
+static const Cfg kCfg[] = {
+  {128, 128, 32, 256, 2, 4},   // 0: C8
+  {128, 128, 16, 512, 2, 2},   // 1: C4
+  {128, 64, 32, 256, 2, 2},    // 2
+  {64, 128, 32, 256, 2, 2},    // 3
+  {64, 64, 32, 512, 2, 2},     // 4
+};
 
-template <int BM, int BN, int WGM, int WGN, bool AK, bool BKc, int TAG>
+template <int BM, int BN, int WGM, int WGN, int BKT, int MINW, bool AK, bool BKc, int TAG>
 static void launch_one(const GemmParams& p, hipStream_t st) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, AK, BKc, TAG>), dim3(tiles, 1, p.nbatch * p.nsplit),
-                     dim3(64 * WGM * WGN), 0, st, p);
+  hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, BKT, MINW, AK, BKc, TAG>),
+                     dim3(tiles, 1, p.nbatch * p.nsplit), dim3(64 * WGM * WGN), 0, st, p);
 }
 
 // Tagged call sites get their own kernel symbol for their one operand layout:
 // 1 exchange contraction (A k-contig, B n-contig), 2 XC forward U (k, k),
 // 3 XC back L (m, n), 4 XC forward W (k, n), 5 XC back M (m, n).
-template <int BM, int BN, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, int BKT, int MINW>
 static void launch_cfg(const GemmParams& p, hipStream_t st, bool akc, bool bkc, int tag) {
-  if (tag == 1 && akc && !bkc) launch_one<BM, BN, WGM, WGN, true, false, 1>(p, st);
-  else if (tag == 2 && akc && bkc) launch_one<BM, BN, WGM, WGN, true, true, 2>(p, st);
-  else if (tag == 3 && !akc && !bkc) launch_one<BM, BN, WGM, WGN, false, false, 3>(p, st);
-  else if (tag == 4 && akc && !bkc) launch_one<BM, BN, WGM, WGN, true, false, 4>(p, st);
-  else if (tag == 5 && !akc && !bkc) launch_one<BM, BN, WGM, WGN, false, false, 5>(p, st);
-  else launch_tag<BM, BN, WGM, WGN, 0>(p, st, akc, bkc);
+  if (tag == 1 && akc && !bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, true, false, 1>(p, st);
+  else if (tag == 2 && akc && bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, true, true, 2>(p, st);
+  else if (tag == 3 && !akc && !bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, false, false, 3>(p, st);
+  else if (tag == 4 && akc && !bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, true, false, 4>(p, st);
+  else if (tag == 5 && !akc && !bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, false, false, 5>(p, st);
+  else if (akc && bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, true, true, 0>(p, st);
+  else if (akc)        launch_one<BM, BN, WGM, WGN, BKT, MINW, true, false, 0>(p, st);
+  else if (bkc)        launch_one<BM, BN, WGM, WGN, BKT, MINW, false, true, 0>(p, st);
+  else                 launch_one<BM, BN, WGM, WGN, BKT, MINW, false, false, 0>(p, st);
 }
 
 size_t dgemm_workspace_bytes(const GemmDesc& d) {
   // mirrors the split choice in dgemm(); callers size their workspace with it
-  GemmParams p; int bm, bn;
-  plan_gemm(d, &p, &bm, &bn);
+  GemmParams p; int cfg;
+  plan_gemm(d, &p, &cfg);
   if (p.nsplit <= 1) return 0;
   return sizeof(double) * (size_t)p.nsplit * p.nbatch * (size_t)p.M * p.N;
 }
 
-void plan_gemm(const GemmDesc& d, GemmParams* pp, int* bm_out, int* bn_out) {
+// Debug / tuning knob: XT_GEMM_CFG=<index into kCfg> forces a configuration.
+static int forced_cfg() {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("XT_GEMM_CFG");
+    v = e ? atoi(e) : -1;
+    if (v >= (int)(sizeof(kCfg) / sizeof(kCfg[0]))) v = -1;
+  }
+  return v;
+}
+
+// Relative MFMA time of a tile with vm valid rows / vn valid cols: the busiest
+// SIMD's share (waves w and w + 4 share a SIMD; MN-edge waves skip their
+// out-of-range 16x16 sub-tiles), 1 for an interior tile.
+static double tile_cost(const Cfg& c, int vm, int vn) {
+  const int WM = c.bm / c.wgm, WN = c.bn / c.wgn, TM = WM / 16, TN = WN / 16;
+  const int nw = c.wgm * c.wgn;
+  double simd[4] = {0, 0, 0, 0};
+  for (int w = 0; w < nw; ++w) {
+    const int wm = w / c.wgn, wn = w % c.wgn;
+    int mi = (vm - wm * WM + 15) / 16, nj = (vn - wn * WN + 15) / 16;
+    mi = mi < 0 ? 0 : (mi > TM ? TM : mi);
+    nj = nj < 0 ? 0 : (nj > TN ? TN : nj);
+    simd[w % 4] += mi * nj;
+  }
+  const double full = (double)((nw + 3) / 4) * TM * TN;
+  double mx = 0;
+  for (double v : simd) mx = v > mx ? v : mx;
+  return mx / full;
+}
+
+// Split-K count: list-schedule the blocks of each candidate split over the
+// chip's concurrent block slots (tile categories interior / M-edge / N-edge /
+// corner, each block = cost x K-tiles + a fixed prologue/epilogue) and add the
+// split-K reduction's HBM time; keep >= 8 K-tiles per split.  Cached per shape.
+static int choose_split(const Cfg& c, int M, int N, long nbatch, long units) {
+  const int tm = (M + c.bm - 1) / c.bm, tn = (N + c.bn - 1) / c.bn;
+  const long tiles = (long)tm * tn * nbatch;
+  if (tiles >= 4L * c.slots || units < 16) return 1;
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int, long, long>, int> cache;
+  const auto key = std::make_tuple((int)(&c - kCfg), M, N, nbatch, units);
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  const int vm = M - (tm - 1) * c.bm, vn = N - (tn - 1) * c.bn;
+  const double cost[4] = {tile_cost(c, c.bm, c.bn), tile_cost(c, vm, c.bn),
+                          tile_cost(c, c.bm, vn), tile_cost(c, vm, vn)};
+  const long cnt[4] = {(long)(tm - 1) * (tn - 1) * nbatch, (long)(tn - 1) * nbatch,
+                       (long)(tm - 1) * nbatch, nbatch};
+  const double t_kt = 2.0 * c.bm * c.bn * c.bk * c.slots / 70e12;   // s per K-tile per block
+  const double t_blk = 2e-6;                                        // prologue + epilogue
+  int best = 1;
+  double best_t = 1e30;
+  for (int s = 1; s <= 64; ++s) {
+    if (s > 1 && units / s < 8) break;
+    if (tiles * s > 32768) break;
+    const long ku = (units + s - 1) / s;
+    std::priority_queue<double, std::vector<double>, std::greater<double>> slots;
+    for (int i = 0; i < c.slots; ++i) slots.push(0.0);
+    double span = 0.0;
+    for (int k = 0; k < 4; ++k)
+      for (long b = 0; b < cnt[k] * s; ++b) {
+        const double t = slots.top() + cost[k] * ku * t_kt + t_blk;
+        slots.pop();
+        slots.push(t);
+        span = t > span ? t : span;
+      }
+    if (s > 1) span += (s + 1.0) * M * N * nbatch * 8.0 / 4e12 + 4e-6;
+    if (span < best_t * 0.995) { best_t = span; best = s; }
+  }
+  std::lock_guard<std::mutex> g(mu);
+  cache[key] = best;
+  return best;
+}
+
+void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
   GemmParams& p = *pp;
   p.M = d.M; p.N = d.N; p.K = d.K; p.R = d.R > 0 ? d.R : 1;
   p.A = d.A; p.sAm = d.sAm; p.sAk = d.sAk; p.sAr = d.sAr; p.sAb1 = d.sAb1; p.sAb2 = d.sAb2;
@@ -359,24 +448,18 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* bm_out, int* bn_out) {
   p.nb2 = d.nb2 > 0 ? d.nb2 : 1;
   p.nbatch = (d.nb1 > 0 ? d.nb1 : 1) * p.nb2;
   p.ws = nullptr;
-  int bm = (d.M >= 96) ? 128 : 64;
-  int bn = (d.N >= 96) ? 128 : 64;
-  // small-M/N problems with few tiles prefer 64-wide tiles for parallelism
-  long tiles = (long)((d.M + bm - 1) / bm) * ((d.N + bn - 1) / bn) * p.nbatch;
-  if (tiles < 256 && bm == 128 && bn == 128) { bn = 64; tiles *= 2; }
-  const long units = (long)p.R * ((d.K + BK - 1) / BK);
-  int nsplit = 1;
-  const long target = 2 * 256;   // 2 blocks per CU
-  if (tiles < target && units >= 16) {
-    long s = (target + tiles - 1) / tiles;
-    long smax = units / 8;      // keep >= 8 K-tiles per split
-    if (s > smax) s = smax;
-    if (s > 64) s = 64;
-    if (s > 1) nsplit = (int)s;
-  }
+  int cfg;
+  if (d.M >= 96 && d.N >= 96) cfg = ((long)p.R * d.K <= 256) ? 1 : 0;
+  else if (d.M >= 96) cfg = 2;
+  else if (d.N >= 96) cfg = 3;
+  else cfg = 4;
+  if (forced_cfg() >= 0) cfg = forced_cfg();
+  const Cfg& c = kCfg[cfg];
+  const long units = (long)p.R * ((d.K + c.bk - 1) / c.bk);
+  int nsplit = choose_split(c, d.M, d.N, p.nbatch, units);
   if (d.max_split > 0 && nsplit > d.max_split) nsplit = d.max_split;
   p.nsplit = nsplit;
-  *bm_out = bm; *bn_out = bn;
+  *cfg_out = cfg;
 }
 
 int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
@@ -387,10 +470,10 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
   if (!bkc && d.sBn != 1) return XT_ERR_ARG;
   // the kernel addresses a tile with 32-bit byte offsets from its origin
   const long lim = 1L << 32;
-  if ((akc ? (128L * d.sAm + BK) : (BK * d.sAk + 128L)) * 8 >= lim) return XT_ERR_ARG;
-  if ((bkc ? (128L * d.sBn + BK) : (BK * d.sBk + 128L)) * 8 >= lim) return XT_ERR_ARG;
-  GemmParams p; int bm, bn;
-  plan_gemm(d, &p, &bm, &bn);
+  if ((akc ? (128L * d.sAm + 32) : (32L * d.sAk + 128L)) * 8 >= lim) return XT_ERR_ARG;
+  if ((bkc ? (128L * d.sBn + 32) : (32L * d.sBk + 128L)) * 8 >= lim) return XT_ERR_ARG;
+  GemmParams p; int cfg;
+  plan_gemm(d, &p, &cfg);
   if (d.K <= 0) {   // C = beta*C
     p.nsplit = 1;
     p.R = 1; p.K = 0;
@@ -406,10 +489,13 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
     }
     p.ws = ws;
   }
-  if (bm == 128 && bn == 128)      launch_cfg<128, 128, 2, 4>(p, st, akc, bkc, d.tag);
-  else if (bm == 128)              launch_cfg<128, 64, 2, 2>(p, st, akc, bkc, d.tag);
-  else if (bn == 128)              launch_cfg<64, 128, 2, 2>(p, st, akc, bkc, d.tag);
-  else                             launch_cfg<64, 64, 2, 2>(p, st, akc, bkc, d.tag);
+  switch (cfg) {
+    case 0: launch_cfg<128, 128, 2, 4, 32, 2>(p, st, akc, bkc, d.tag); break;
+    case 1: launch_cfg<128, 128, 2, 2, 16, 2>(p, st, akc, bkc, d.tag); break;
+    case 2: launch_cfg<128, 64, 2, 2, 32, 1>(p, st, akc, bkc, d.tag); break;
+    case 3: launch_cfg<64, 128, 2, 2, 32, 1>(p, st, akc, bkc, d.tag); break;
+    default: launch_cfg<64, 64, 2, 2, 32, 2>(p, st, akc, bkc, d.tag); break;
+  }
   if (p.nsplit > 1) {
     long total = (long)p.nbatch * p.M * p.N;
     int blocks = (int)((total + 255) / 256);

@@ -37,7 +37,7 @@ struct GemmParams {
   double* ws;
 };
 
-void plan_gemm(const GemmDesc& d, GemmParams* p, int* bm, int* bn);
+void plan_gemm(const GemmDesc& d, GemmParams* p, int* cfg);
 size_t dgemm_workspace_bytes(const GemmDesc& d);
 int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes);
 
