@@ -209,6 +209,25 @@ dgemm_kernel(GemmParams p) {
     constexpr bool k_edge = decltype(K_EDGE)::value;
     const int abase = buf * STAGE + (wm * WM + r16) * LDP + q;
     const int bbase = buf * STAGE + BM * LDP + (wn * WN + r16) * LDP + q;
+    if constexpr (MINW >= 4) {
+      // >= 4 waves per SIMD hide the LDS latency across waves: single-buffered
+      // fragments keep the wave inside a 128-register budget
+#pragma unroll
+      for (int s = 0; s < SK; ++s) {
+        double af1[TM], bf1[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af1[i] = smem[abase + i * 16 * LDP + 4 * s];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bf1[j] = smem[bbase + j * 16 * LDP + 4 * s];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            if ((!k_edge || 4 * s < kv) && (!mn_edge || (i < mi && j < nj)))
+              acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af1[i], bf1[j], acc[i][j], 0, 0, 0);
+      }
+      return;
+    }
     double af[2][TM], bf[2][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i) af[0][i] = smem[abase + i * 16 * LDP];
@@ -317,9 +336,9 @@ __global__ void splitk_reduce(GemmParams p) {
 }
 
 // Tile configurations.  C8: 128x128, 8 waves (64x32 each), BK 32, one block
-// per CU (135 KB LDS).  C4: 128x128, 4 waves (64x64 each), BK 16, two blocks
-// per CU (70 KB LDS each) so one block's barrier / prologue / epilogue hides
-// under the other's MFMAs.  Narrow tiles for small M or N.
+// per CU (135 KB LDS); with BK 16 (70 KB) two such blocks share a CU, so one
+// block's barrier / prologue / epilogue hides under the other's MFMAs.
+// C4: 4 waves of 64x64.  Narrow tiles for small M or N.
 struct Cfg { int bm, bn, bk, slots, wgm, wgn; };
 static const Cfg kCfg[] = {
   {128, 128, 32, 256, 2, 4},   // 0: C8
@@ -327,6 +346,8 @@ static const Cfg kCfg[] = {
   {128, 64, 32, 256, 2, 2},    // 2
   {64, 128, 32, 256, 2, 2},    // 3
   {64, 64, 32, 512, 2, 2},     // 4
+  {128, 128, 16, 512, 2, 4},   // 5: C8 with BK 16, two blocks per CU
+  {256, 128, 16, 256, 4, 2},   // 6: 256x128, 8 waves of 64x64, BK 16 (tuning only)
 };
 
 template <int BM, int BN, int WGM, int WGN, int BKT, int MINW, bool AK, bool BKc, int TAG>
@@ -449,7 +470,11 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
   p.nbatch = (d.nb1 > 0 ? d.nb1 : 1) * p.nb2;
   p.ws = nullptr;
   int cfg;
-  if (d.M >= 96 && d.N >= 96) cfg = ((long)p.R * d.K <= 256) ? 1 : 0;
+  // 128x128: two 8-wave blocks per CU (BK 16, 128-register budget) except for
+  // the (m-contiguous A, n-contiguous B) layout, which spills there and runs
+  // one 8-wave block per CU with BK 32 (measured, tools/gemm_bench.py)
+  const bool ff = (d.sAk != 1) && (d.sBk != 1);
+  if (d.M >= 96 && d.N >= 96) cfg = ff ? 0 : 5;
   else if (d.M >= 96) cfg = 2;
   else if (d.N >= 96) cfg = 3;
   else cfg = 4;
@@ -470,8 +495,8 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
   if (!bkc && d.sBn != 1) return XT_ERR_ARG;
   // the kernel addresses a tile with 32-bit byte offsets from its origin
   const long lim = 1L << 32;
-  if ((akc ? (128L * d.sAm + 32) : (32L * d.sAk + 128L)) * 8 >= lim) return XT_ERR_ARG;
-  if ((bkc ? (128L * d.sBn + 32) : (32L * d.sBk + 128L)) * 8 >= lim) return XT_ERR_ARG;
+  if ((akc ? (256L * d.sAm + 32) : (32L * d.sAk + 256L)) * 8 >= lim) return XT_ERR_ARG;
+  if ((bkc ? (256L * d.sBn + 32) : (32L * d.sBk + 256L)) * 8 >= lim) return XT_ERR_ARG;
   GemmParams p; int cfg;
   plan_gemm(d, &p, &cfg);
   if (d.K <= 0) {   // C = beta*C
@@ -494,6 +519,8 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
     case 1: launch_cfg<128, 128, 2, 2, 16, 2>(p, st, akc, bkc, d.tag); break;
     case 2: launch_cfg<128, 64, 2, 2, 32, 1>(p, st, akc, bkc, d.tag); break;
     case 3: launch_cfg<64, 128, 2, 2, 32, 1>(p, st, akc, bkc, d.tag); break;
+    case 5: launch_cfg<128, 128, 2, 4, 16, 4>(p, st, akc, bkc, d.tag); break;
+    case 6: launch_cfg<256, 128, 4, 2, 16, 2>(p, st, akc, bkc, d.tag); break;
     default: launch_cfg<64, 64, 2, 2, 32, 2>(p, st, akc, bkc, d.tag); break;
   }
   if (p.nsplit > 1) {
