@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define XT_ABI_VERSION 1
+#define XT_ABI_VERSION 2
 
 #define XT_PTR_HOST 0
 #define XT_PTR_DEVICE 1
@@ -77,6 +77,24 @@ int xt_set_orbital_energies(xt_ctx* ctx, const double* e_a, const double* e_b, i
    Replaces mf.get_jk / get_j / get_k (XTDA.py:518-543, SF_TDA.py:273-281,
    XSF_TDA.py:996) -- the AO->MO transform is done once here on the device. */
 int xt_set_jk_df(xt_ctx* ctx, const double* cderi, int which, int ptr_kind);
+/* Stored 4-index ERIs instead of a DF factor (jk_mode ERI8): PySCF 8-fold
+   packed order ('s8', ao2mo.restore(8, ...)): pair index ij = i(i+1)/2 + j
+   (i >= j), npair = nao(nao+1)/2, (ij|kl) stored at ij(ij+1)/2 + kl (ij >= kl).
+   Factorised on the device by pivoted Cholesky, (mu nu|la si) = sum_P L_P L_P,
+   down to a largest residual diagonal <= tol (tol <= 0: 1e-13 x the largest
+   diagonal), i.e. exact to that tolerance; the Cholesky vectors then drive the
+   same MO-route J/K engine as xt_set_jk_df.  The context keeps the vectors of
+   the contiguous block p_rank of p_count (multi-GPU aux sharding; 0, 1 for
+   all) and takes that count as its naux (xt_naux); a long-range set (which = 1)
+   of a different rank is zero-padded to a common naux.
+   Replaces the incore mf._eri consumed by PySCF get_jk / get_k(omega=)
+   (XTDA.py:518-543, SF_TDA.py:273-281, XSF_TDA.py:857,996). */
+int xt_set_jk_eri8(xt_ctx* ctx, const double* eri_s8, int which, double tol,
+                   int p_rank, int p_count, int ptr_kind);
+/* DF / Cholesky functions held by this context (desc.naux, or the rank
+   found by xt_set_jk_eri8) and the full Cholesky rank of the last
+   xt_set_jk_eri8 (before sharding). */
+int xt_naux(const xt_ctx* ctx, int* naux_local, int* chol_rank);
 /* AO values on the grid (ncomp x ngrid x nao; ncomp = 1 LDA / 4 GGA),
    weights (ngrid) and the kernel: UKS fxc (2 x ncomp x 2 x ncomp x ngrid,
    un-weighted) for XTDA/UTDA, or the weighted ALDA0 kernel (ngrid) for SF/XSF.

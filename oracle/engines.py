@@ -54,6 +54,33 @@ def get_jk(cderi, dms, with_j=True, with_k=True):
     return vj, vk
 
 
+def unpack_eri_s8(packed, nao):
+    """PySCF 8-fold packed ERIs -> full (nao,)*4, written out with explicit
+    loops over the pair indices (ao2mo.restore(1, eri, nao) semantics):
+    ij = i(i+1)/2 + j (i >= j), (ij|kl) at ij(ij+1)/2 + kl (ij >= kl)."""
+    full = np.empty((nao, nao, nao, nao))
+    pairs = [(i, j) for i in range(nao) for j in range(i + 1)]
+    for ij, (i, j) in enumerate(pairs):
+        for kl, (k, l) in enumerate(pairs[:ij + 1]):
+            v = packed[ij * (ij + 1) // 2 + kl]
+            for a, b in ((i, j), (j, i)):
+                for c, d in ((k, l), (l, k)):
+                    full[a, b, c, d] = v
+                    full[c, d, a, b] = v
+    return full
+
+
+def get_jk_eri(eri_full, dms, with_j=True, with_k=True):
+    """PySCF incore get_jk convention on a full 4-index tensor:
+    vj = einsum('ijkl,kl->ij', eri, dm), vk = einsum('ijkl,jk->il', eri, dm)."""
+    dms = np.asarray(dms, dtype=np.float64)
+    shape = dms.shape
+    d = dms.reshape(-1, shape[-2], shape[-1])
+    vj = np.einsum('ijkl,xkl->xij', eri_full, d).reshape(shape) if with_j else None
+    vk = np.einsum('ijkl,xjk->xil', eri_full, d).reshape(shape) if with_k else None
+    return vj, vk
+
+
 def get_k_total(mf, dms):
     """Exchange with the functional's hybrid coefficients (already scaled)."""
     c_full, c_lr = _k_coeffs(mf)

@@ -130,3 +130,59 @@ def test_sharded_contexts_sum_to_full_operator(dev):
     vind, hdiag = o.gen_tda_operation_sf(fglobal=fg)
     z = make_trial_vectors(4, hdiag.size)
     assert rel(parts[0].apply(z) + parts[1].apply(z), vind(z)) < RTOL
+
+
+# ---- stored ERIs (jk_mode ERI8): device pivoted Cholesky + the DF engine ----
+ERI8_TOL = 1e-11   # Cholesky to 1e-13 x max diagonal: exact to round-off at these sizes
+
+
+@pytest.mark.parametrize("case", ["xtda_gga", "xtda_rsh", "utda_lda", "sf_down", "sf_up", "xsf_sa"])
+def test_eri8_equals_df(dev, case):
+    """ERI8 (the packed ERIs sum_P B B) and DF (B) on the same tensor agree, and
+    both match the oracle (the two modes test each other)."""
+    from xtddft_amd.synthetic import as_eri8
+    kw, o = {}, None
+    if case == "xtda_gga":
+        mf, kind = make_mf(nao=24, nc=4, no=2, xctype="GGA"), "XTDA"
+        vind = oxtda.gen_tda_operation(mf)[0]
+    elif case == "xtda_rsh":
+        mf, kind = make_mf(nao=24, nc=4, no=2, xctype="GGA", omega=0.33, alpha=0.65, hyb=0.19), "XTDA"
+        vind = oxtda.gen_tda_operation(mf)[0]
+    elif case == "utda_lda":
+        mf, kind = make_mf(nao=24, nc=4, no=2, xctype="LDA", kind="U"), "UTDA"
+        vind = oxtda.gen_tda_operation(mf)[0]
+    elif case in ("sf_down", "sf_up"):
+        mf = make_mf(nao=24, nc=4, no=2, xctype="GGA", hyb=0.5)
+        isf = -1 if case == "sf_down" else 1
+        kind = "SF_DOWN" if isf == -1 else "SF_UP"
+        vind = osf.gen_tda_operation_sf(mf, isf)[0]
+    else:
+        mf, kind = make_mf(nao=24, nc=4, no=3, xctype="GGA", hyb=0.5), "XSF"
+        o = oxsf.XSFOracle(mf, SA=2)
+        kw = dict(sa=2, fglobal=oxsf.default_fglobal(mf), foo=0.7, remove=o.re)
+        vind = o.gen_tda_operation_sf(foo=0.7, fglobal=kw["fglobal"])[0]
+    op_df, op_eri = dev(mf, kind, **kw), dev(as_eri8(mf), kind, **kw)
+    if o is not None:
+        op_df.set_oo_basis(o.vects)
+        op_eri.set_oo_basis(o.vects)
+    z = make_trial_vectors(5, op_df.dim)
+    s_df, s_eri = op_df.apply(z), op_eri.apply(z)
+    assert rel(s_eri, s_df) < ERI8_TOL
+    assert rel(s_eri, vind(z)) < ERI8_TOL
+    naux, rank = op_eri.naux()
+    assert rank == mf.naux and naux == mf.naux   # synthetic B has full column rank naux < npair
+    if kind == "XSF":
+        co, ov = op_eri.xsf_j_diagonals()
+        co_ref, ov_ref = op_df.xsf_j_diagonals()
+        assert np.abs(co - co_ref).max() < 1e-12 and np.abs(ov - ov_ref).max() < 1e-12
+
+
+def test_eri8_sharded_cholesky_sums_to_full(dev):
+    """Aux sharding of the Cholesky vectors (multi-GPU): the
+    per-rank partial sigma (one-electron terms on rank 0) sum to the full sigma."""
+    from xtddft_amd.synthetic import as_eri8
+    mf = as_eri8(make_mf(nao=24, nc=4, no=2, xctype="GGA", omega=0.33, alpha=0.65, hyb=0.19))
+    z = make_trial_vectors(4, dev(mf, "XTDA").dim)
+    full = dev(mf, "XTDA").apply(z)
+    parts = [dev(mf, "XTDA", shard=(r, 3)).apply(z) for r in range(3)]
+    assert rel(sum(parts), full) < 1e-13

@@ -27,7 +27,7 @@ def test_library_builds_and_exports_every_header_symbol(hiplib):
     assert len(syms) >= 20
     for s in syms:
         assert hasattr(hiplib, s), s
-    assert hiplib.xt_abi_version() == 1
+    assert hiplib.xt_abi_version() == 2
 
 
 def test_desc_layout_matches_c_header(tmp_path):
@@ -123,3 +123,44 @@ def test_no_cpu_fallback_in_product():
         if f.endswith(".py"):
             src = open(os.path.join(pkg, f)).read()
             assert "import oracle" not in src and "from oracle" not in src, f
+
+
+# ---- stored-ERI (jk_mode ERI8) host side -----------------------------------
+def test_eri_s8_packing_matches_pyscf_convention():
+    """xtddft_amd.eri packing == the loop-written ao2mo 's8' convention of the oracle."""
+    from oracle.engines import unpack_eri_s8
+    from xtddft_amd import eri as E
+    rng = np.random.default_rng(3)
+    nao = 6
+    b = rng.standard_normal((9, nao, nao))
+    b = b + b.transpose(0, 2, 1)
+    full = np.einsum('pij,pkl->ijkl', b, b)
+    packed = E.pack_s8(full)
+    assert packed.size == E.npair(nao) * (E.npair(nao) + 1) // 2
+    assert np.array_equal(unpack_eri_s8(packed, nao), E.unpack_s8(packed, nao))
+    assert np.abs(unpack_eri_s8(packed, nao) - full).max() < 1e-13
+    assert np.abs(E.eri_from_cderi(b) - packed).max() < 1e-12
+
+
+def test_oracle_eri_jk_equals_df_jk():
+    """The stored-ERI J/K (PySCF get_jk convention) on sum_P B B equals the DF J/K on B,
+    for non-symmetric densities (hermi = 0, XTDA.py:518-543)."""
+    from oracle.engines import get_jk, get_jk_eri, unpack_eri_s8
+    from xtddft_amd.synthetic import as_eri8, make_mf
+    mf = make_mf(nao=10, nc=3, no=2, xctype="HF")
+    full = unpack_eri_s8(as_eri8(mf).eri, 10)
+    dms = np.random.default_rng(4).standard_normal((3, 10, 10))
+    vj, vk = get_jk(mf.cderi, dms)
+    vj2, vk2 = get_jk_eri(full, dms)
+    assert np.abs(vj - vj2).max() < 1e-13 and np.abs(vk - vk2).max() < 1e-13
+
+
+def test_meanfield_eri_validation():
+    import dataclasses
+    from xtddft_amd.synthetic import as_eri8, make_mf
+    mf = as_eri8(make_mf(nao=8, nc=2, no=2, xctype="HF"))
+    assert mf.jk_mode == "ERI8" and mf.naux == 0
+    with pytest.raises(ValueError):
+        dataclasses.replace(mf, eri=mf.eri[:-1])
+    with pytest.raises(ValueError):
+        dataclasses.replace(mf, eri=None)

@@ -23,6 +23,7 @@ ERRORS = {-1: ValueError, -2: MemoryError, -3: RuntimeError, -4: RuntimeError, -
 EXPORTS = [
     "xt_create", "xt_destroy", "xt_set_stream", "xt_last_error", "xt_abi_version",
     "xt_set_orbitals", "xt_set_fock_mo", "xt_set_orbital_energies", "xt_set_jk_df",
+    "xt_set_jk_eri8", "xt_naux",
     "xt_set_grid", "xt_set_oo_basis", "xt_apply", "xt_dim", "xt_last_timings",
     "xt_xsf_j_diagonals", "xt_set_profile", "xt_profile_stats", "xt_dgemm", "xt_precond", "xt_row_norms2", "xt_row_scale",
 ]
@@ -36,6 +37,9 @@ class XtDesc(ctypes.Structure):
         ("si", c_double), ("sa", c_int), ("foo", c_double), ("fglobal", c_double),
         ("remove", c_int), ("add_local", c_int), ("device", c_int),
     ]
+
+
+ABI_VERSION = 2   # include/xtddft_amd.h XT_ABI_VERSION
 
 
 class LibraryMissing(RuntimeError):
@@ -73,6 +77,8 @@ def lib():
     L.xt_set_fock_mo.argtypes = [vp, dp, dp, dp, dp, c_int]
     L.xt_set_orbital_energies.argtypes = [vp, dp, dp, c_int]
     L.xt_set_jk_df.argtypes = [vp, dp, c_int, c_int]
+    L.xt_set_jk_eri8.argtypes = [vp, dp, c_int, c_double, c_int, c_int, c_int]
+    L.xt_naux.argtypes = [vp, POINTER(c_int), POINTER(c_int)]
     L.xt_set_grid.argtypes = [vp, dp, dp, dp, c_int]
     L.xt_set_oo_basis.argtypes = [vp, dp, c_int]
     L.xt_apply.argtypes = [vp, c_int, dp, dp, c_int]
@@ -89,6 +95,8 @@ def lib():
     for name in EXPORTS:
         if not hasattr(L, name):
             raise LibraryMissing(f"{LIB_PATH} lacks symbol {name}")
+    if L.xt_abi_version() != ABI_VERSION:
+        raise LibraryMissing(f"{LIB_PATH} has ABI {L.xt_abi_version()}, expected {ABI_VERSION}; rebuild")
     _lib = L
     return L
 

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_lib")
 OUT = os.path.join(OUT_DIR, "libxtddft_amd.so")
-SOURCES = ["xt_gemm.hip", "xt_kernels.hip", "xt_ctx.hip"]
+SOURCES = ["xt_gemm.hip", "xt_kernels.hip", "xt_chol.hip", "xt_ctx.hip"]
 HEADERS = ["xt_internal.h", "xt_kernels.h", "../../include/xtddft_amd.h"]
 ARCH = os.environ.get("XT_OFFLOAD_ARCH", "gfx950")
 

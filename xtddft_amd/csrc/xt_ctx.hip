@@ -17,6 +17,7 @@
 // the reference's AO route (the projections are linear), different summation
 // order: parity is to FP64 round-off, see tests/test_gpu_parity.py.
 #include <hip/hip_runtime.h>
+#include <utility>
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
@@ -51,6 +52,12 @@ struct DevBuf {
   void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
 };
 
+// function-local scratch: freed on every return path
+struct TmpBuf : DevBuf {
+  ~TmpBuf() { release(); }
+  void swap(DevBuf& o) { std::swap(p, o.p); std::swap(n, o.n); }
+};
+
 struct xt_ctx {
   xt_desc d;
   hipStream_t st = nullptr;
@@ -74,6 +81,7 @@ struct xt_ctx {
   double prof_flops[6] = {0, 0, 0, 0, 0, 0};
   double prof_ms[6] = {0, 0, 0, 0, 0, 0};
   int prof_launches[6] = {0, 0, 0, 0, 0, 0};
+  int chol_rank = 0;         // full Cholesky rank of the last xt_set_jk_eri8
 };
 
 static int dim_of(const xt_desc& d) {
@@ -273,22 +281,26 @@ int xt_set_orbital_energies(xt_ctx* c, const double* ea, const double* eb, int p
 }
 
 // Bmo[b][P] = C_b^T B_P C_b, chunked over P so host inputs stream through HBM.
-int xt_set_jk_df(xt_ctx* c, const double* cderi, int which, int ptr_kind) {
-  if (!c || !cderi) return fail(XT_ERR_ARG, "null argument");
-  if (!c->has_orb) return fail(XT_ERR_STATE, "xt_set_orbitals must precede xt_set_jk_df");
-  (void)hipSetDevice(c->d.device);
-  const int nao = c->d.nao, nmo = c->d.nmo, naux = c->d.naux;
+// AO factor rows (np x nao x nao) -> MO factor Bmo[b][P] = C_b^T B_P C_b for
+// P < np, rows np..naux_rows of each basis block zeroed (dst holds
+// nbasis x naux_rows x nmo x nmo).
+static int df_to_mo(xt_ctx* c, const double* cderi, int np_total, DevBuf& dst, int naux_rows, int ptr_kind) {
+  const int nao = c->d.nao, nmo = c->d.nmo;
   const size_t mm = (size_t)nmo * nmo, aa = (size_t)nao * nao;
-  DevBuf& dst = which == 0 ? c->Bmo : c->Bmo_lr;
-  RET(dst.ensure(mm * naux * c->nbasis));
+  RET(dst.ensure(mm * (size_t)naux_rows * c->nbasis));
+  if (naux_rows > np_total)
+    for (int b = 0; b < c->nbasis; ++b)
+      HIPCHK(hipMemsetAsync(dst.p + ((size_t)b * naux_rows + np_total) * mm, 0,
+                            (size_t)(naux_rows - np_total) * mm * 8, c->st));
+  if (np_total <= 0) return 0;
   const size_t budget = (size_t)2 << 30;   // bytes per staging buffer
   int pc = (int)(budget / (8 * (aa > mm ? aa : mm)));
   if (pc < 1) pc = 1;
-  if (pc > naux) pc = naux;
+  if (pc > np_total) pc = np_total;
   RET(c->stage2.ensure((size_t)pc * nao * nmo));
   if (ptr_kind == XT_PTR_HOST) RET(c->stage.ensure((size_t)pc * aa));
-  for (int p0 = 0; p0 < naux; p0 += pc) {
-    const int np = (p0 + pc <= naux) ? pc : naux - p0;
+  for (int p0 = 0; p0 < np_total; p0 += pc) {
+    const int np = (p0 + pc <= np_total) ? pc : np_total - p0;
     const double* src = cderi + (size_t)p0 * aa;
     if (ptr_kind == XT_PTR_HOST) {
       HIPCHK(hipMemcpyAsync(c->stage.p, src, (size_t)np * aa * 8, hipMemcpyHostToDevice, c->st));
@@ -306,13 +318,114 @@ int xt_set_jk_df(xt_ctx* c, const double* cderi, int which, int ptr_kind) {
       g2.M = nmo; g2.N = nmo; g2.K = nao; g2.nb1 = np;
       g2.A = Cb; g2.sAm = 1; g2.sAk = nmo;
       g2.B = c->stage2.p; g2.sBk = nmo; g2.sBn = 1; g2.sBb1 = (long)nao * nmo;
-      g2.C = dst.p + ((size_t)b * naux + p0) * mm; g2.ldc = nmo; g2.sCb1 = (long)mm;
+      g2.C = dst.p + ((size_t)b * naux_rows + p0) * mm; g2.ldc = nmo; g2.sCb1 = (long)mm;
       RET(gemm(c, g2));
     }
   }
+  return 0;
+}
+
+int xt_set_jk_df(xt_ctx* c, const double* cderi, int which, int ptr_kind) {
+  if (!c || !cderi) return fail(XT_ERR_ARG, "null argument");
+  if (which != 0 && which != 1) return fail(XT_ERR_ARG, "which must be 0 (full range) or 1 (long range)");
+  if (!c->has_orb) return fail(XT_ERR_STATE, "xt_set_orbitals must precede xt_set_jk_df");
+  (void)hipSetDevice(c->d.device);
+  DevBuf& dst = which == 0 ? c->Bmo : c->Bmo_lr;
+  RET(df_to_mo(c, cderi, c->d.naux, dst, c->d.naux, ptr_kind));
   HIPCHK(hipStreamSynchronize(c->st));
   c->stage.release(); c->stage2.release();
   if (which == 0) c->has_df = true; else c->has_lr = true;
+  return 0;
+}
+
+// Re-lay an MO factor (nbasis blocks of old_rows x mm) with new_rows >= old_rows
+// rows per block, the extra rows zero.
+static int grow_factor(xt_ctx* c, DevBuf& B, int old_rows, int new_rows) {
+  const size_t mm = (size_t)c->d.nmo * c->d.nmo;
+  TmpBuf nb;
+  RET(nb.ensure((size_t)c->nbasis * new_rows * mm));
+  HIPCHK(hipMemsetAsync(nb.p, 0, nb.n * 8, c->st));
+  for (int b = 0; b < c->nbasis; ++b)
+    if (old_rows > 0)
+      HIPCHK(hipMemcpyAsync(nb.p + (size_t)b * new_rows * mm, B.p + (size_t)b * old_rows * mm,
+                            (size_t)old_rows * mm * 8, hipMemcpyDeviceToDevice, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  nb.swap(B);   // B takes the new rows, nb frees the old ones
+  return 0;
+}
+
+int xt_set_jk_eri8(xt_ctx* c, const double* eri, int which, double tol, int p_rank, int p_count, int ptr_kind) {
+  if (!c || !eri) return fail(XT_ERR_ARG, "null argument");
+  if (which != 0 && which != 1) return fail(XT_ERR_ARG, "which must be 0 (full range) or 1 (long range)");
+  if (p_count < 1 || p_rank < 0 || p_rank >= p_count) return fail(XT_ERR_ARG, "bad shard (p_rank, p_count)");
+  if (!c->has_orb) return fail(XT_ERR_STATE, "xt_set_orbitals must precede xt_set_jk_eri8");
+  (void)hipSetDevice(c->d.device);
+  const int nao = c->d.nao;
+  const long npair = (long)nao * (nao + 1) / 2;
+  const size_t n8 = (size_t)npair * (npair + 1) / 2;
+  const double* e = eri;
+  TmpBuf ebuf, d, Lt, piv, Bao;
+  if (ptr_kind == XT_PTR_HOST) {
+    RET(ebuf.ensure(n8));
+    HIPCHK(hipMemcpyAsync(ebuf.p, eri, n8 * 8, hipMemcpyHostToDevice, c->st));
+    e = ebuf.p;
+  }
+  RET(d.ensure(npair));
+  RET(piv.ensure(2));
+  eri_diag(c->st, npair, e, d.p);
+  long cap = 8L * nao < npair ? 8L * nao : npair;
+  RET(Lt.ensure((size_t)cap * npair));
+  double thr = tol;
+  int rank = 0;
+  for (; rank < npair; ++rank) {
+    argmax(c->st, npair, d.p, piv.p);
+    double hv[2];
+    HIPCHK(hipMemcpyAsync(hv, piv.p, 16, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (rank == 0 && thr <= 0.0) thr = 1e-13 * hv[0];
+    if (!(hv[0] > thr)) break;
+    if (rank == cap) {   // grow the vector store
+      const long ncap = 2 * cap < npair ? 2 * cap : npair;
+      TmpBuf nl;
+      RET(nl.ensure((size_t)ncap * npair));
+      HIPCHK(hipMemcpyAsync(nl.p, Lt.p, (size_t)cap * npair * 8, hipMemcpyDeviceToDevice, c->st));
+      HIPCHK(hipStreamSynchronize(c->st));
+      nl.swap(Lt);
+      cap = ncap;
+    }
+    chol_step(c->st, npair, rank, (long)hv[1], hv[0], e, Lt.p, npair, d.p);
+  }
+  ebuf.release(); d.release(); piv.release();
+  // this rank's contiguous block of Cholesky vectors
+  const int base = rank / p_count, rem = rank % p_count;
+  const int lo = p_rank * base + (p_rank < rem ? p_rank : rem);
+  const int np = base + (p_rank < rem ? 1 : 0);
+  if (np > 0) {
+    RET(Bao.ensure((size_t)np * nao * nao));
+    chol_unpack(c->st, np, lo, nao, Lt.p, npair, Bao.p);
+  }
+  // common naux for the full-range and long-range factors (zero-padded)
+  const bool other_set = which == 0 ? c->has_lr : c->has_df;
+  int rows = np;
+  if (other_set) {
+    if (c->d.naux > rows) rows = c->d.naux;
+    else if (c->d.naux < rows) RET(grow_factor(c, which == 0 ? c->Bmo_lr : c->Bmo, c->d.naux, rows));
+  }
+  DevBuf& dst = which == 0 ? c->Bmo : c->Bmo_lr;
+  dst.release();
+  RET(df_to_mo(c, Bao.p, np, dst, rows, XT_PTR_DEVICE));
+  HIPCHK(hipStreamSynchronize(c->st));
+  Bao.release(); Lt.release(); c->stage.release(); c->stage2.release();
+  c->d.naux = rows;
+  c->chol_rank = rank;
+  if (which == 0) c->has_df = true; else c->has_lr = true;
+  return 0;
+}
+
+int xt_naux(const xt_ctx* c, int* naux_local, int* chol_rank) {
+  if (!c) return fail(XT_ERR_ARG, "null argument");
+  if (naux_local) *naux_local = c->d.naux;
+  if (chol_rank) *chol_rank = c->chol_rank;
   return 0;
 }
 

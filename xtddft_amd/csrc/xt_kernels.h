@@ -26,4 +26,10 @@ void xsf_jdiag(hipStream_t st, int naux, int nmo, int nc, int no, int nv, const 
 void precond(hipStream_t st, int nrow, int dim, const double* diag, const double* e, double shift, const double* r, double* out);
 void row_norms2(hipStream_t st, int nrow, int dim, const double* x, double* out);
 void row_scale(hipStream_t st, int nrow, int dim, double* x, const double* s);
+// pivoted Cholesky of packed 8-fold ERIs (xt_chol.hip)
+void eri_diag(hipStream_t st, long npair, const double* eri, double* d);
+void argmax(hipStream_t st, long n, const double* d, double* out2);
+void chol_step(hipStream_t st, long npair, int k, long p, double dp, const double* eri, double* Lt, long ldL,
+               double* d);
+void chol_unpack(hipStream_t st, int np, int p0, int nao, const double* Lt, long ldL, double* B);
 }  // namespace xt

@@ -68,9 +68,15 @@ class MeanField:
     veff     : (2, nao, nao)  KS effective potential at the SCF density.
     veff_hf  : (2, nao, nao)  pure-HF potential at the same density
                (``scf.ROHF(mol).get_veff(mol, dm)``, XTDA.py:608-612).
-    cderi    : (naux, nao, nao) symmetric DF factor, full-range Coulomb.
+    cderi    : (naux, nao, nao) symmetric DF factor, full-range Coulomb
+               (jk_mode 'DF').
     cderi_lr : optional (naux, nao, nao) factor of the long-range
                erf(omega r)/r operator for range-separated hybrids.
+    eri      : stored 4-index ERIs in PySCF 8-fold packed order (the incore
+               ``mf._eri``, ``ao2mo.restore(8, ...)``) -- jk_mode 'ERI8',
+               used when ``cderi`` is None.  ``eri_lr`` likewise for the
+               long-range operator; ``chol_tol`` the device Cholesky
+               tolerance (0: 1e-13 x largest diagonal).
     fxc      : (2, ncomp, 2, ncomp, ngrid) un-weighted UKS second derivative
                kernel (``cache_xc_kernel`` output, XTDA.py:504).
     fxc_sf   : (ngrid,) ALDA0 spin-flip kernel already multiplied by the grid
@@ -85,7 +91,7 @@ class MeanField:
     h1e: np.ndarray
     veff: np.ndarray
     veff_hf: np.ndarray
-    cderi: np.ndarray
+    cderi: Optional[np.ndarray] = None
     grids: Optional[Grid] = None
     fxc: Optional[np.ndarray] = None
     fxc_sf: Optional[np.ndarray] = None
@@ -96,6 +102,9 @@ class MeanField:
     alpha: float = 0.0
     hyb: float = 0.0
     level_shift: float = 0.0
+    eri: Optional[np.ndarray] = None
+    eri_lr: Optional[np.ndarray] = None
+    chol_tol: float = 0.0
     e_tot: float = 0.0
     max_memory: int = 4000
     extra: dict = field(default_factory=dict)
@@ -116,8 +125,16 @@ class MeanField:
                                      np.zeros(occ.size - nc - no)])
             if not np.array_equal(occ, expect):
                 raise ValueError("ROKS mo_occ must be ordered core|open|virtual")
-        if self.cderi.ndim != 3 or self.cderi.shape[1:] != (self.nao, self.nao):
+        if self.cderi is None and self.eri is None:
+            raise ValueError("need a DF factor (cderi) or stored ERIs (eri)")
+        if self.cderi is not None and (self.cderi.ndim != 3 or self.cderi.shape[1:] != (self.nao, self.nao)):
             raise ValueError("cderi must be (naux, nao, nao)")
+        npair = self.nao * (self.nao + 1) // 2
+        for name in ("eri", "eri_lr"):
+            e = getattr(self, name)
+            if e is not None and np.asarray(e).size != npair * (npair + 1) // 2:
+                raise ValueError(f"{name} must be 8-fold packed: npair*(npair+1)/2 = "
+                                 f"{npair * (npair + 1) // 2} elements for nao = {self.nao}")
 
     # ---- reference attribute surface -------------------------------------
     @property
@@ -129,8 +146,12 @@ class MeanField:
         return int(self.mo_coeff.shape[-2])
 
     @property
+    def jk_mode(self) -> str:
+        return "DF" if self.cderi is not None else "ERI8"
+
+    @property
     def naux(self) -> int:
-        return int(self.cderi.shape[0])
+        return int(self.cderi.shape[0]) if self.cderi is not None else 0
 
     def get_hcore(self):
         return self.h1e

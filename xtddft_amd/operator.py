@@ -79,6 +79,7 @@ class DeviceOperator:
         self.nc, self.no, self.nv = nc, no, nv
         naux = mf.naux
         ngrid = mf.grids.ngrid if (mf.grids is not None and mf.xctype != "HF") else 0
+        self.shard = (rank, nranks)
         if presharded:
             self.aux_range, self.grid_range = (0, naux), (0, ngrid)
         else:
@@ -129,7 +130,17 @@ class DeviceOperator:
             _capi.check(L.xt_set_orbital_energies(h, e[0][0], e[1][0], _capi.XT_PTR_HOST),
                         "xt_set_orbital_energies")
         p0, p1 = self.aux_range
-        if p1 > p0:
+        if mf.jk_mode == "ERI8":
+            # stored ERIs: factorised on the device; this rank keeps its block
+            # of Cholesky vectors (aux sharding)
+            rank, nranks = self.shard
+            for which, eri in ((0, mf.eri), (1, mf.eri_lr if mf.omega != 0 else None)):
+                if eri is None:
+                    continue
+                pe, ke, re_ = _ptr(eri)
+                _capi.check(L.xt_set_jk_eri8(h, pe, which, float(mf.chol_tol), rank, nranks, ke),
+                            "xt_set_jk_eri8")
+        elif p1 > p0:
             pc, kc, rc = _ptr(mf.cderi[p0:p1])
             _capi.check(L.xt_set_jk_df(h, pc, 0, kc), "xt_set_jk_df")
             if mf.cderi_lr is not None and mf.omega != 0:
@@ -147,6 +158,12 @@ class DeviceOperator:
             if not (kao == kw == kk):
                 raise TypeError("grid arrays must all be host or all device")
             _capi.check(L.xt_set_grid(h, pao, pw, pk, kao), "xt_set_grid")
+
+    def naux(self):
+        """(DF / Cholesky functions on this rank, full Cholesky rank of an ERI8 factorisation)."""
+        a, r = ctypes.c_int(), ctypes.c_int()
+        _capi.check(self._L.xt_naux(self._h, ctypes.byref(a), ctypes.byref(r)), "xt_naux")
+        return a.value, r.value
 
     def set_oo_basis(self, vects):
         p, k, r = _ptr(vects)

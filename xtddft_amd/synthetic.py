@@ -164,6 +164,17 @@ def make_mf(nao=24, nc=5, no=2, naux=None, ngrid=None, xctype="GGA", hyb=0.2,
                      omega=omega, alpha=alpha, hyb=hyb)
 
 
+def as_eri8(mf: MeanField, chol_tol: float = 0.0) -> MeanField:
+    """The same mean field in jk_mode 'ERI8': the DF factor(s) replaced by the
+    8-fold packed ERIs they define, (mu nu|la si) = sum_P B B (SURVEY.md 8(d):
+    DF and ERI8 are fed the same tensor so the two modes test each other)."""
+    import dataclasses
+    from .eri import eri_from_cderi
+    eri_lr = eri_from_cderi(mf.cderi_lr) if mf.cderi_lr is not None else None
+    return dataclasses.replace(mf, cderi=None, cderi_lr=None, eri=eri_from_cderi(mf.cderi),
+                               eri_lr=eri_lr, chol_tol=chol_tol)
+
+
 def make_device_mf(nao=1000, nc=99, no=2, naux=None, ngrid=None, xctype="GGA", hyb=0.2,
                    seed=DEFAULT_SEED, device=0, shard=(0, 1)) -> MeanField:
     """Synthetic ROKS problem whose big tensors are generated directly in HBM.
