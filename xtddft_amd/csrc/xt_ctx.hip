@@ -113,8 +113,9 @@ static int gemm(xt_ctx* c, const GemmDesc& g) {
     }
     c->pev_tag[c->pev_used] = g.tag;
     HIPCHK(hipEventRecord(c->pev[c->pev_used], c->st));
-    c->prof_flops[g.tag] += 2.0 * g.M * (double)g.N * g.K * (g.R > 0 ? g.R : 1) *
-                            (g.nb1 > 0 ? g.nb1 : 1) * (g.nb2 > 0 ? g.nb2 : 1);
+    c->prof_flops[g.tag] += g.flops > 0 ? g.flops
+                                         : 2.0 * g.M * (double)g.N * g.K * (g.R > 0 ? g.R : 1) *
+                                               (g.nb1 > 0 ? g.nb1 : 1) * (g.nb2 > 0 ? g.nb2 : 1);
   }
   size_t need = dgemm_workspace_bytes(g);
   if (need > 0) {
@@ -670,8 +671,14 @@ static int exchange_main(xt_ctx* c, int nz, const DevBuf& B, double coef) {
 
 // ---------------------------------------------------------------------------
 // XC response over the grid (chunks of G points), W route (see k_xc_uks_w):
-//   F1 U = PhiV0 Ze^T ; F2 W = PhiO0 Zp (GGA) ; point kernel ; B1 acc += L^T PhiV0 ;
-//   B2 accT += PhiO0^T M (GGA).  LDA / ALDA0: F1, point kernel, B1.
+//   F1  U = PhiV0 Ze^T                              (GEMM, tag 2)
+//   F2' rhoW[g][xg][c] = sum_a (PhiO0 Zp)[g,xg,a] dPhiV_c[g,a]
+//                                                   (fused GEMM mode 1, tag 4: W never stored)
+//   point kernel: rho = U-part + rhoW; wv; U <- L; rhoW <- wv[1..3]
+//   B1  acc += L^T PhiV0                            (GEMM, tag 3)
+//   B2' accT += PhiO0^T M, M[g,xg,a] = sum_c wv_c dPhiV_c[g,a] generated on the fly
+//                                                   (fused GEMM mode 2, tag 5: M never stored)
+// LDA / ALDA0: F1, point kernel, B1.
 // ---------------------------------------------------------------------------
 static int xc_response(xt_ctx* c, int nz) {
   const int O = c->O, V = c->V, nmo = c->d.nmo, ng = c->d.ngrid, nc = c->ncomp;
@@ -680,21 +687,22 @@ static int xc_response(xt_ctx* c, int nz) {
   const long chs = (long)nz * O * V;
   Group gr[2];
   const int ngr = channel_groups(c, gr);
-  const size_t per_g = (size_t)nch * nz * O + (gga ? (size_t)nch * nz * V : 0);
-  size_t G = ((size_t)4 << 30) / (8 * per_g);
+  const size_t per_g = (size_t)nch * nz * O + (gga ? (size_t)nch * nz * 3 : 0);
+  size_t G = ((size_t)8 << 30) / (8 * per_g);
   if (G > (size_t)ng) G = ng;
   if (G < 64) G = 64 < (size_t)ng ? 64 : ng;
   RET(c->ubuf.ensure((size_t)nch * nz * O * G));
-  if (gga) RET(c->wbuf.ensure((size_t)nch * nz * V * G));
+  if (gga) RET(c->wbuf.ensure((size_t)nch * nz * 3 * G));
   const long compP = (long)ng * nmo;
   const long basP = (long)nc * compP;
+  const int nab = (V + 15) / 16;
   for (int g0 = 0; g0 < ng; g0 += (int)G) {
     const int n = (g0 + (int)G <= ng) ? (int)G : ng - g0;
-    double* Ug[2]; double* Wg[2]; long ldU[2], ldW[2];
+    double* Ug[2]; double* Rg[2]; long ldU[2], ldR[2];
     for (int q = 0; q < ngr; ++q) {
       const int nzg = gr[q].nch * nz;
       Ug[q] = c->ubuf.p + (long)gr[q].ch0 * nz * O * n;  ldU[q] = (long)nzg * O;
-      Wg[q] = gga ? c->wbuf.p + (long)gr[q].ch0 * nz * V * n : nullptr;  ldW[q] = (long)nzg * V;
+      Rg[q] = gga ? c->wbuf.p + (long)gr[q].ch0 * nz * 3 * n : nullptr;  ldR[q] = (long)nzg * 3;
       const double* PV = c->Phi.p + gr[q].vb * basP + (long)g0 * nmo + c->v0;
       const double* PO = c->Phi.p + gr[q].ob * basP + (long)g0 * nmo;
       GemmDesc f1;   // U[g][(x,i)] = sum_a PhiV0[g][a] Ze[(x,i)][a]
@@ -705,28 +713,30 @@ static int xc_response(xt_ctx* c, int nz) {
       f1.tag = 2;
       RET(gemm(c, f1));
       if (gga) {
-        GemmDesc f2;   // W[g][(x,a)] = sum_i PhiO0[g][i] Zp[i][(x,a)]
-        f2.M = n; f2.N = nzg * V; f2.K = O;
-        f2.A = PO; f2.sAm = nmo; f2.sAk = 1;
-        f2.B = c->zp.p + gr[q].ch0 * chs; f2.sBk = (long)nzg * V; f2.sBn = 1;
-        f2.C = Wg[q]; f2.ldc = ldW[q];
+        GemmDesc f2;   // rhoW[g][xg][c] = sum_a sum_i PhiO0[g][i] Zp[i][xg][a] dPhiV_c[g][a]
+        f2.M = 16 * nzg; f2.N = n; f2.K = O; f2.R = nab;
+        f2.A = c->zp.p + gr[q].ch0 * chs; f2.sAm = 1; f2.sAk = (long)nzg * V; f2.sAr = 16;
+        f2.B = PO; f2.sBk = 1; f2.sBn = nmo;
+        f2.fz.mode = 1; f2.fz.ablk = V; f2.fz.V = V; f2.fz.nx = nzg;
+        f2.fz.w = PV + compP; f2.fz.wc = compP; f2.fz.wg = nmo;
+        f2.fz.rho = Rg[q]; f2.fz.rg = ldR[q];
         f2.tag = 4;
+        f2.flops = 2.0 * nzg * V * (double)n * O;
         RET(gemm(c, f2));
       }
     }
     if (nch == 2) {
       // spin s -> (group, row offset inside the group)
-      double* Us[2]; double* Ws[2]; long lus[2], lws[2];
+      double* Us[2]; double* Rs[2]; long lus[2], lrs[2];
       for (int s = 0; s < 2; ++s) {
         const int q = (ngr == 1) ? 0 : s;
         const int off = (ngr == 1) ? s : 0;
         Us[s] = Ug[q] + (long)off * nz * O; lus[s] = ldU[q];
-        Ws[s] = gga ? Wg[q] + (long)off * nz * V : nullptr; lws[s] = ldW[q];
+        Rs[s] = gga ? Rg[q] + (long)off * nz * 3 : nullptr; lrs[s] = ldR[q];
       }
-      xc_uks_w(c->st, nc, n, g0, ng, nz, O, V, nmo, c->v0, compP,
+      xc_uks_w(c->st, nc, n, g0, ng, nz, O, nmo, compP,
                c->Phi.p + c->occ_basis[0] * basP, c->Phi.p + c->occ_basis[1] * basP,
-               c->Phi.p + c->vir_basis[0] * basP, c->Phi.p + c->vir_basis[1] * basP,
-               c->kern.p, Us[0], lus[0], Us[1], lus[1], Ws[0], lws[0], Ws[1], lws[1]);
+               c->kern.p, Us[0], lus[0], Us[1], lus[1], Rs[0], lrs[0], Rs[1], lrs[1]);
     } else {
       xc_sf(c->st, n, g0, nz, O, nmo, c->Phi.p + c->occ_basis[0] * basP, c->kern.p, Ug[0]);
     }
@@ -742,12 +752,16 @@ static int xc_response(xt_ctx* c, int nz) {
       b1.tag = 3;
       RET(gemm(c, b1));
       if (gga) {
-        GemmDesc b2;   // accT[i][(x,a)] += sum_g PhiO0[g][i] M[g][(x,a)]
-        b2.M = O; b2.N = nzg * V; b2.K = n;
+        GemmDesc b2;   // accT[i][(xg,a)] += sum_g PhiO0[g][i] sum_c wv_c[g][xg] dPhiV_c[g][a]
+        const int nxb = (nzg + 7) / 8;
+        b2.M = O; b2.N = nxb * nab * 128; b2.K = n;
         b2.A = PO; b2.sAm = 1; b2.sAk = nmo;
-        b2.B = Wg[q]; b2.sBk = ldW[q]; b2.sBn = 1;
+        b2.fz.mode = 2; b2.fz.V = V; b2.fz.nx = nzg;
+        b2.fz.w = PV + compP; b2.fz.wc = compP; b2.fz.wg = nmo;
+        b2.fz.rho = Rg[q]; b2.fz.rg = ldR[q];
         b2.C = c->accT.p + gr[q].ch0 * chs; b2.ldc = (long)nzg * V; b2.beta = 1.0;
         b2.tag = 5;
+        b2.flops = 2.0 * O * (double)nzg * V * n;
         RET(gemm(c, b2));
       }
     }
@@ -879,7 +893,10 @@ extern "C" int xt_apply(xt_ctx* c, int nz, const double* z, double* sigma, int p
   else if (xsf) xsf_assemble(c->st, nz, d.nc, d.no, d.nv, d.remove, c->vects.p, zd, c->ze.p);
   else HIPCHK(hipMemcpyAsync(c->ze.p, zd, chs * 8, hipMemcpyDeviceToDevice, c->st));
   HIPCHK(hipMemsetAsync(c->acc.p, 0, nch * chs * 8, c->st));
-  RET(c->zp.ensure(nch * chs));
+  // Zp gets 32 zeroed doubles of slack: the fused rho-forward GEMM reads whole
+  // 16-wide a-blocks, up to 15 past the last channel's V (weighted by zero)
+  RET(c->zp.ensure(nch * chs + 32));
+  HIPCHK(hipMemsetAsync(c->zp.p + nch * chs, 0, 32 * 8, c->st));
   RET(c->accT.ensure(nch * chs));
   HIPCHK(hipMemsetAsync(c->accT.p, 0, nch * chs * 8, c->st));
   Group grp[2];

@@ -48,13 +48,19 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // group reads row r at k = q + 4s, i.e. dword 2*(LDP*r + q) mod 32, which is
 // conflict-free for any odd pitch.  Odd pitch also keeps both staging stores
 // (16 consecutive k of one row, or one k of 16 consecutive rows) conflict-free.
+// Kernel-local lambdas capture register arrays (accumulators, staging) by
+// reference: they must inline, or the arrays are demoted to scratch memory.
+#define XT_INLINE __attribute__((always_inline))
 constexpr int GROUP_M = 8;       // m-tiles per grouped sweep over n (L2 panel reuse)
 
 // TAG only gives hot call sites their own kernel symbol (rocprofv3 identity).
 // MINW = waves per SIMD the register budget must allow (occupancy target).
-template <int BM, int BN, int WGM, int WGN, int BK, int MINW, bool A_KC, bool B_KC, int TAG>
+// MODE: 0 plain GEMM, 1 / 2 fused XC contractions (XcFuse, xt_internal.h).
+template <int BM, int BN, int WGM, int WGN, int BK, int MINW, bool A_KC, bool B_KC, int TAG, int MODE = 0>
 __global__ void __launch_bounds__(64 * WGM * WGN, MINW)
 dgemm_kernel(GemmParams p) {
+  static_assert(MODE == 0 || (BM == 128 && BN == 128 && WGM == 2 && WGN == 4 && !A_KC && B_KC),
+                "fused XC modes run on the 128x128 8-wave tile, A MN-contiguous, B staged K-contiguous");
   constexpr int LDP = BK + 1;
   constexpr int NTHREADS = 64 * WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;    // wave tile
@@ -104,13 +110,16 @@ dgemm_kernel(GemmParams p) {
 
   const int m0 = tm * BM, n0 = tn * BN;
   const int nkt = (p.K + BK - 1) / BK;
+  // mode 2: n-tile tn covers xg-block tn % nxb (8 xg) x a-block tn / nxb (16 a)
+  const int nxb = (p.fz.nx + 7) / 8;
+  const int xg_blk = MODE == 2 ? tn % nxb : 0, a_blk = MODE == 2 ? tn / nxb : 0;
   const long units = (long)p.R * nkt;
   const long u_per = (units + p.nsplit - 1) / p.nsplit;
   const long u0 = split * u_per;
   const long u1 = (u0 + u_per < units) ? (u0 + u_per) : units;
 
   const double* __restrict__ Ab = p.A + b1 * p.sAb1 + b2 * p.sAb2 +
-                                  (A_KC ? (long)m0 * p.sAm : (long)m0);
+                                  (MODE == 1 ? 0L : (A_KC ? (long)m0 * p.sAm : (long)m0));
   const double* __restrict__ Bb = p.B + b1 * p.sBb1 + b2 * p.sBb2 +
                                   (B_KC ? (long)n0 * p.sBn : (long)n0);
 
@@ -128,14 +137,18 @@ dgemm_kernel(GemmParams p) {
   const int b_fix = B_KC ? tid % BK : tid % BN, b_var = B_KC ? tid / BK : tid / BN;
   unsigned aoff[A_ELEMS], boff[B_ELEMS];
   unsigned a_row0, b_row0;   // MN-contiguous operands: offset of k-row 0 (k-edge fallback)
+  // mode 1 rows m = 16 xg + a_l sit at xg * ablk + a_l (the a-block via r * sAr)
+  auto rowoff = [&](int mg) XT_INLINE -> long {
+    return MODE == 1 ? (long)(mg >> 4) * p.fz.ablk + (mg & 15) : (long)(mg - m0);
+  };
 #pragma unroll
   for (int e = 0; e < A_ELEMS; ++e) {
     if (A_KC) {
       int mm = min(m0 + a_var + e * A_STEP, p.M - 1) - m0;
       aoff[e] = (unsigned)(((long)mm * p.sAm + a_fix) * 8);
     } else {
-      int mm = min(m0 + a_fix, p.M - 1) - m0;
-      aoff[e] = (unsigned)(((long)(a_var + e * A_STEP) * p.sAk + mm) * 8);
+      const long mo = rowoff(min(m0 + a_fix, p.M - 1));
+      aoff[e] = (unsigned)(((long)(a_var + e * A_STEP) * p.sAk + mo) * 8);
     }
   }
 #pragma unroll
@@ -148,7 +161,20 @@ dgemm_kernel(GemmParams p) {
       boff[e] = (unsigned)(((long)(b_var + e * B_STEP) * p.sBk + nn) * 8);
     }
   }
-  a_row0 = (unsigned)((min(m0 + a_fix, p.M - 1) - m0) * 8);
+  a_row0 = (unsigned)(rowoff(min(m0 + a_fix, p.M - 1)) * 8);
+  // mode 2: this thread's fixed virtual index a (column % 16) and per-element xg
+  const int a_gen = a_blk * 16 + (b_var & 15);
+  const bool a_ok = a_gen < p.fz.V;
+  const int a_cl = a_ok ? a_gen : p.fz.V - 1;
+  if (MODE == 2) {
+#pragma unroll
+    for (int e = 0; e < B_ELEMS; ++e) {
+      const int xg = xg_blk * 8 + (b_var + e * B_STEP) / 16;
+      boff[e] = (unsigned)((xg < p.fz.nx ? xg : p.fz.nx - 1) * 3);   // rho offset (doubles)
+    }
+  }
+  double bw[MODE == 2 ? 3 : 1];                    // mode 2: w_c[g][a] of the staged k row
+  double br[MODE == 2 ? B_ELEMS : 1][3];           // mode 2: rho[g][xg_e][c]
   b_row0 = (unsigned)((min(n0 + b_fix, p.N - 1) - n0) * 8);
 
   double ra[A_ELEMS], rb[B_ELEMS];
@@ -156,7 +182,7 @@ dgemm_kernel(GemmParams p) {
   // Stage K-tile (r, kt) into registers.  Branch-free: k past K (last tile of
   // each r) reads k = 0 of the same row instead; the B copy of those k is
   // zeroed in store_tile, so they add nothing.  Returns the valid k count.
-  auto load_tile = [&](int r, int kt) -> int {
+  auto load_tile = [&](int r, int kt) XT_INLINE -> int {
     const int k0 = kt * BK;
     const int kv = p.K - k0;
     const char* At = (const char*)(Ab + (long)r * p.sAr + (A_KC ? (long)k0 : (long)k0 * p.sAk));
@@ -168,16 +194,27 @@ dgemm_kernel(GemmParams p) {
       else      o = (a_var + e * A_STEP < kv) ? aoff[e] : a_row0;
       ra[e] = *(const double*)(At + o);
     }
+    if constexpr (MODE == 2) {
+      // generated operand: raw inputs of k row g (clamped to the tile's first row past K)
+      const long g = k0 + (b_fix < kv ? b_fix : 0);
 #pragma unroll
-    for (int e = 0; e < B_ELEMS; ++e) {
-      unsigned o;
-      if (B_KC) o = (b_fix < kv) ? boff[e] : boff[e] - (unsigned)(b_fix * 8);
-      else      o = (b_var + e * B_STEP < kv) ? boff[e] : b_row0;
-      rb[e] = *(const double*)(Bt + o);
+      for (int c = 0; c < 3; ++c) bw[c] = p.fz.w[c * p.fz.wc + g * p.fz.wg + a_cl];
+#pragma unroll
+      for (int e = 0; e < B_ELEMS; ++e)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) br[e][c] = p.fz.rho[g * p.fz.rg + boff[e] + c];
+    } else {
+#pragma unroll
+      for (int e = 0; e < B_ELEMS; ++e) {
+        unsigned o;
+        if (B_KC) o = (b_fix < kv) ? boff[e] : boff[e] - (unsigned)(b_fix * 8);
+        else      o = (b_var + e * B_STEP < kv) ? boff[e] : b_row0;
+        rb[e] = *(const double*)(Bt + o);
+      }
     }
     return kv;
   };
-  auto store_tile = [&](int buf, int kv) {
+  auto store_tile = [&](int buf, int kv) XT_INLINE {
 #pragma unroll
     for (int e = 0; e < A_ELEMS; ++e) {
       int mm, kk;
@@ -188,7 +225,15 @@ dgemm_kernel(GemmParams p) {
     for (int e = 0; e < B_ELEMS; ++e) {
       int nn, kk;
       if (B_KC) { nn = b_var + e * B_STEP; kk = b_fix; } else { kk = b_var + e * B_STEP; nn = b_fix; }
-      smem[buf * STAGE + BM * LDP + nn * LDP + kk] = (kk < kv) ? rb[e] : 0.0;
+      double v;
+      if constexpr (MODE == 2) {
+        const int xg = xg_blk * 8 + nn / 16;
+        v = br[e][0] * bw[0] + br[e][1] * bw[1] + br[e][2] * bw[2];
+        v = (a_ok && xg < p.fz.nx && kk < kv) ? v : 0.0;
+      } else {
+        v = (kk < kv) ? rb[e] : 0.0;
+      }
+      smem[buf * STAGE + BM * LDP + nn * LDP + kk] = v;
     }
   };
   // MFMA sub-tiles of this wave that hold any row < M / col < N; a wave whose
@@ -204,7 +249,7 @@ dgemm_kernel(GemmParams p) {
   // never stored); K_EDGE: skip k-steps wholly past K (their B rows are zero).
   // Fragment reads stay unconditional (LDS holds clamped rows), so the read
   // pipelining is identical in every variant.
-  auto compute = [&](int buf, auto MN_EDGE, auto K_EDGE, int kv) {
+  auto compute = [&](int buf, auto MN_EDGE, auto K_EDGE, int kv) XT_INLINE {
     constexpr bool mn_edge = decltype(MN_EDGE)::value;
     constexpr bool k_edge = decltype(K_EDGE)::value;
     const int abase = buf * STAGE + (wm * WM + r16) * LDP + q;
@@ -257,7 +302,7 @@ dgemm_kernel(GemmParams p) {
   // skips the k-steps past K.  Waves whose sub-tiles reach past M / N run the
   // MN_EDGE variant of the same loop (wave-uniform choice; both variants pass
   // the same barriers).
-  auto run = [&](auto MN_EDGE) {
+  auto run = [&](auto MN_EDGE) XT_INLINE {
     int r = (int)(u0 / nkt), kt = (int)(u0 % nkt);
     int kv = load_tile(r, kt);
     store_tile(0, kv);
@@ -279,12 +324,99 @@ dgemm_kernel(GemmParams p) {
     }
     compute(buf, MN_EDGE, std::true_type{}, p.K - kt * BK);
   };
-  if (u0 < u1) {
-    if (wave_full) run(std::false_type{});
-    else           run(std::true_type{});
+  if constexpr (MODE == 1) {
+    // rho forward: one a-block (16 a of 8 xg) per r; after its last K-tile the
+    // accumulators (W for 128 grid points) are contracted with the gradient
+    // weights and reduced over a; lane q keeps xg_l = 4 wm + q.
+    static_assert(TM == 4, "lane-q ownership of the 4 row sub-tiles");
+    double racc[TN][3];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) racc[j][c] = 0.0;
+    auto rho_epilogue = [&](int r) XT_INLINE {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int g = min(n0 + wn * WN + j * 16 + r16, p.N - 1);
+        double w[3][4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int a = 16 * r + q + 4 * t;
+          const bool ok = a < p.fz.V;
+          const int acl = ok ? a : p.fz.V - 1;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const double wv = p.fz.w[c * p.fz.wc + (long)g * p.fz.wg + acl];
+            w[c][t] = ok ? wv : 0.0;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            double sv = acc[i][j][0] * w[c][0] + acc[i][j][1] * w[c][1] + acc[i][j][2] * w[c][2] +
+                        acc[i][j][3] * w[c][3];
+            sv += __shfl_xor(sv, 16);
+            sv += __shfl_xor(sv, 32);
+            if (q == i) racc[j][c] += sv;
+          }
+          acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+        }
+      }
+    };
+    auto run1 = [&](auto MN_EDGE) XT_INLINE {
+      int kv = load_tile(0, 0);
+      store_tile(0, kv);
+      __syncthreads();
+      int buf = 0;
+      for (int r = 0; r < p.R; ++r) {
+        for (int kt = 0; kt + 1 < nkt; ++kt) {
+          kv = load_tile(r, kt + 1);
+          compute(buf, MN_EDGE, std::false_type{}, BK);
+          __builtin_amdgcn_sched_barrier(0);
+          store_tile(buf ^ 1, kv);
+          __syncthreads();
+          buf ^= 1;
+        }
+        kv = load_tile(r + 1 < p.R ? r + 1 : r, 0);   // first tile of the next a-block
+        compute(buf, MN_EDGE, std::true_type{}, p.K - (nkt - 1) * BK);
+        __builtin_amdgcn_sched_barrier(0);
+        store_tile(buf ^ 1, kv);
+        __syncthreads();
+        buf ^= 1;
+        rho_epilogue(r);
+      }
+    };
+    if (nkt > 0) {
+      if (wave_full) run1(std::false_type{});
+      else           run1(std::true_type{});
+    }
+    const int xg = (m0 >> 4) + wm * TM + q;
+    if (xg < p.fz.nx) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int g = n0 + wn * WN + j * 16 + r16;
+        if (g < p.N)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) p.fz.rho[(long)g * p.fz.rg + 3 * xg + c] = racc[j][c];
+      }
+    }
+    return;
+  } else {
+    if (u0 < u1) {
+      if (wave_full) run(std::false_type{});
+      else           run(std::true_type{});
+    }
   }
 
   // ---- epilogue ------------------------------------------------------------
+  // mode 2: logical column n -> C column xg V + a (-1: padding, not stored)
+  auto ccol = [&](int nl) XT_INLINE -> long {
+    if (MODE != 2) return nl;
+    const int c = nl - n0;
+    const int xg = xg_blk * 8 + c / 16, a = a_blk * 16 + (c & 15);
+    return (xg < p.fz.nx && a < p.fz.V) ? (long)xg * p.fz.V + a : -1L;
+  };
   if (p.nsplit > 1) {
     double* W = p.ws + ((long)split * p.nbatch + b) * (long)p.M * p.N;
 #pragma unroll
@@ -307,8 +439,9 @@ dgemm_kernel(GemmParams p) {
         for (int t = 0; t < 4; ++t) {
           int gm = m0 + wm * WM + i * 16 + q + 4 * t;
           int gn = n0 + wn * WN + j * 16 + r16;
-          if (gm < p.M && gn < p.N) {
-            double* c = Cb + (long)gm * p.ldc + gn;
+          const long cn = ccol(gn);
+          if (gm < p.M && gn < p.N && cn >= 0) {
+            double* c = Cb + (long)gm * p.ldc + cn;
             double v = p.alpha * acc[i][j][t];
             if (p.beta != 0.0) v += p.beta * (*c);
             *c = v;
@@ -325,10 +458,17 @@ __global__ void splitk_reduce(GemmParams p) {
     const int b = (int)(idx / mn);
     const long e = idx % mn;
     const int m = (int)(e / p.N), n = (int)(e % p.N);
+    long cn = n;
+    if (p.fz.mode == 2) {   // logical column -> xg V + a (see dgemm_kernel mode 2)
+      const int nxb = (p.fz.nx + 7) / 8, tn = n / 128, cc = n % 128;
+      const int xg = (tn % nxb) * 8 + cc / 16, a = (tn / nxb) * 16 + (cc & 15);
+      if (xg >= p.fz.nx || a >= p.fz.V) continue;
+      cn = (long)xg * p.fz.V + a;
+    }
     double s = 0.0;
     for (int sp = 0; sp < p.nsplit; ++sp) s += p.ws[((long)sp * p.nbatch + b) * mn + e];
     const int b1 = b / p.nb2, b2 = b % p.nb2;
-    double* c = p.C + b1 * p.sCb1 + b2 * p.sCb2 + (long)m * p.ldc + n;
+    double* c = p.C + b1 * p.sCb1 + b2 * p.sCb2 + (long)m * p.ldc + cn;
     double v = p.alpha * s;
     if (p.beta != 0.0) v += p.beta * (*c);
     *c = v;
@@ -350,10 +490,10 @@ static const Cfg kCfg[] = {
   {256, 128, 16, 256, 4, 2},   // 6: 256x128, 8 waves of 64x64, BK 16 (tuning only)
 };
 
-template <int BM, int BN, int WGM, int WGN, int BKT, int MINW, bool AK, bool BKc, int TAG>
+template <int BM, int BN, int WGM, int WGN, int BKT, int MINW, bool AK, bool BKc, int TAG, int MODE = 0>
 static void launch_one(const GemmParams& p, hipStream_t st) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, BKT, MINW, AK, BKc, TAG>),
+  hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, BKT, MINW, AK, BKc, TAG, MODE>),
                      dim3(tiles, 1, p.nbatch * p.nsplit), dim3(64 * WGM * WGN), 0, st, p);
 }
 
@@ -469,6 +609,15 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
   p.nb2 = d.nb2 > 0 ? d.nb2 : 1;
   p.nbatch = (d.nb1 > 0 ? d.nb1 : 1) * p.nb2;
   p.ws = nullptr;
+  p.fz = d.fz;
+  if (d.fz.mode != 0) {   // fused XC modes: fixed 128x128 8-wave BK 32 tile
+    const Cfg& c = kCfg[0];
+    const long units = (long)p.R * ((d.K + c.bk - 1) / c.bk);
+    p.nsplit = d.fz.mode == 1 ? 1 : choose_split(c, d.M, d.N, p.nbatch, units);
+    if (d.max_split > 0 && p.nsplit > d.max_split) p.nsplit = d.max_split;
+    *cfg_out = 0;
+    return;
+  }
   int cfg;
   // 128x128: two 8-wave blocks per CU (BK 16, 128-register budget) except for
   // the (m-contiguous A, n-contiguous B) layout, which spills there and runs
@@ -489,8 +638,13 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
 
 int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
   if (d.M <= 0 || d.N <= 0) return 0;
-  const bool akc = (d.sAk == 1);
-  const bool bkc = (d.sBk == 1);
+  const int mode = d.fz.mode;
+  if (mode != 0 && (d.sAm != 1 || d.fz.w == nullptr || d.fz.rho == nullptr || d.fz.nx <= 0 || d.fz.V <= 0))
+    return XT_ERR_ARG;
+  if (mode == 1 && (d.sBk != 1 || d.nb1 > 1 || d.nb2 > 1 || d.M != 16 * d.fz.nx)) return XT_ERR_ARG;
+  if (mode == 2 && (d.R > 1 || d.nb1 > 1 || d.nb2 > 1 || d.N % 128 != 0)) return XT_ERR_ARG;
+  const bool akc = mode == 0 && (d.sAk == 1);
+  const bool bkc = mode != 0 || (d.sBk == 1);
   if (!akc && d.sAm != 1) return XT_ERR_ARG;
   if (!bkc && d.sBn != 1) return XT_ERR_ARG;
   // the kernel addresses a tile with 32-bit byte offsets from its origin
@@ -514,7 +668,11 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
     }
     p.ws = ws;
   }
-  switch (cfg) {
+  if (mode == 1) {
+    launch_one<128, 128, 2, 4, 32, 2, false, true, 4, 1>(p, st);
+  } else if (mode == 2) {
+    launch_one<128, 128, 2, 4, 32, 2, false, true, 5, 2>(p, st);
+  } else switch (cfg) {
     case 0: launch_cfg<128, 128, 2, 4, 32, 2>(p, st, akc, bkc, d.tag); break;
     case 1: launch_cfg<128, 128, 2, 2, 16, 2>(p, st, akc, bkc, d.tag); break;
     case 2: launch_cfg<128, 64, 2, 2, 32, 1>(p, st, akc, bkc, d.tag); break;

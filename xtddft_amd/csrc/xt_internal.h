@@ -12,6 +12,23 @@
 
 namespace xt {
 
+// Fused XC grid contractions (GEMM modes, xt_gemm.hip).  Spin-channel x trial
+// vector pairs xg < nx, virtual index a < V, grid point g.
+//  mode 1 "rho forward":  rows m = 16 xg + a_l, reduce index r = a-block (a = 16 r + a_l),
+//    A(r, m, k) = A[k sAk + xg ablk + 16 r + a_l]  (W = PhiO Zp, never stored);
+//    out: rho[g rg + 3 xg + c] = sum_a W[g, xg, a] w[c wc + g wg + a]   (c < 3)
+//  mode 2 "M backward":   B(g, n) generated as sum_c rho[g rg + 3 xg + c] w[c wc + g wg + a]
+//    with n -> (xg, a) in 8 x 16 blocks (xg-block fastest); C column xg V + a.
+struct XcFuse {
+  int mode = 0;
+  const double* w = nullptr;   // weights (grid gradients of the virtual MOs)
+  long wc = 0, wg = 0;
+  double* rho = nullptr;       // mode 1 output / mode 2 input, (g, xg, 3)
+  long rg = 0;
+  long ablk = 0;               // mode 1: A offset between consecutive xg
+  int V = 0, nx = 0;
+};
+
 // Public-facing GEMM description (see xt_gemm.hip for the contraction).
 struct GemmDesc {
   int M = 0, N = 0, K = 0, R = 1;
@@ -25,6 +42,8 @@ struct GemmDesc {
   double alpha = 1.0, beta = 0.0;
   int max_split = 0;                  // 0 = heuristic
   int tag = 0;                        // kernel identity for profiling (see xt_gemm.hip)
+  double flops = 0.0;                 // algorithmic flops for profiling (0: 2 M N K R batch)
+  XcFuse fz;                          // fused XC mode (fz.mode != 0)
 };
 
 struct GemmParams {
@@ -35,6 +54,7 @@ struct GemmParams {
   double* C; long ldc, sCb1, sCb2;
   double alpha, beta;
   double* ws;
+  XcFuse fz;
 };
 
 void plan_gemm(const GemmDesc& d, GemmParams* p, int* cfg);

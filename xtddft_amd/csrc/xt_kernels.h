@@ -14,10 +14,9 @@ void xsf_rank1(hipStream_t st, int nz, int nc, int no, int nv, int nmo, double a
 void ediag(hipStream_t st, int nz, int O, int V, int nmo, int v0, const double* eps, const double* ze, double* acc);
 void xc_uks(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, int nmo,
             const double* phi0, const double* phi1, const double* wfxc, double* U);
-void xc_uks_w(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, int V, int nmo, int v0,
-              long compP, const double* pO0, const double* pO1, const double* pV0, const double* pV1,
-              const double* wfxc, double* U0, long ldU0, double* U1, long ldU1,
-              double* W0, long ldW0, double* W1, long ldW1);
+void xc_uks_w(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
+              const double* pO0, const double* pO1, const double* wfxc, double* U0, long ldU0,
+              double* U1, long ldU1, double* R0, long ldR0, double* R1, long ldR1);
 void xc_sf(hipStream_t st, int G, int g0, int nz, int O, int nmo, const double* phio, const double* fsf, double* U);
 void weight_fxc(hipStream_t st, long n4, int ngrid, const double* w, double* f);
 void xsf_assemble(hipStream_t st, int nz, int nc, int no, int nv, int remove, const double* vects, const double* z, double* ze);

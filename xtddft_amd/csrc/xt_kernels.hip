@@ -264,48 +264,38 @@ k_xc_uks(int G, int g0, int ngrid, int nz, int O, int nmo,
 
 // ---- XC response, "W route" (one 256-thread block per grid point g) ---------
 // Spin channel s of trial vector x holds, at grid point g (g0 + g globally):
-//   U_s[g][x*O + i] = sum_a PhiV0[g][a] Z[x][i][a]      (GEMM, xc forward)
-//   W_s[g][x*V + a] = sum_i PhiO0[g][i] Z[x][i][a]      (GEMM, GGA only)
+//   U_s[g][x*O + i] = sum_a PhiV0[g][a] Z[x][i][a]       (GEMM, xc forward)
+//   R_s[g][3x + c-1] = sum_a W[g][x][a] PhiVc[g][a]      (fused GEMM, GGA only;
+//                      W[g][x][a] = sum_i PhiO0[g][i] Z[x][i][a] is never stored)
 // and this kernel forms (PySCF eval_rho for a non-hermitian dm + nr_uks_fxc):
-//   rho1[s][0] = sum_i U PhiO0 ;  rho1[s][c] = sum_i U PhiOc + sum_a W PhiVc
+//   rho1[s][0] = sum_i U PhiO0 ;  rho1[s][c] = sum_i U PhiOc + R_s[c-1]
 //   wv[s][y]   = sum_{t,y'} (w fxc)[t,y'][s,y] rho1[t][y']
-//   U <- L = wv0 PhiO0 + sum_c wvc PhiOc ;  W <- M = sum_c wvc PhiVc
-// so that sigma += L^T PhiV0 + PhiO0^T M (two GEMMs, xc back).  The grid point's
-// MO values / gradients and the 2NC x 2NC kernel block are staged once in LDS
-// and reused by all 2*nz vectors.  The kernel streams U/W in and L/M out
-// (HBM-bound): each wave handles one x for both spins and keeps
-// 2 x XW_UNR independent 8-byte loads per lane in flight over the W rows.
-constexpr int XW_UNR = 8;
+//   U <- L = wv0 PhiO0 + sum_c wvc PhiOc ;  R_s <- wv[s][1..3]
+// so that sigma += L^T PhiV0 + PhiO0^T M with M = sum_c wvc PhiVc generated
+// inside the back GEMM.  The grid point's occupied MO values / gradients and
+// the 2NC x 2NC kernel block are staged once in LDS and reused by all 2*nz
+// vectors; each wave handles one x for both spins (HBM-bound on U / L).
 template <int NC>
 __global__ void __launch_bounds__(256, 4)
-k_xc_uks_w(int g0, int ngrid, int nz, int O, int V, int nmo, int v0, long compP,
+k_xc_uks_w(int g0, int ngrid, int nz, int O, int nmo, long compP,
            const double* __restrict__ pO0, const double* __restrict__ pO1,
-           const double* __restrict__ pV0, const double* __restrict__ pV1,
            const double* __restrict__ wfxc,
            double* __restrict__ U0, long ldU0, double* __restrict__ U1, long ldU1,
-           double* __restrict__ W0, long ldW0, double* __restrict__ W1, long ldW1) {
+           double* __restrict__ R0, long ldR0, double* __restrict__ R1, long ldR1) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   __shared__ double sk[4 * NC * NC];   // sk[((t*NC + y')*2 + s)*NC + y] = (w fxc) at this point
   const int g = blockIdx.x;
   const long gg = g0 + g;
   const bool same = (pO0 == pO1);
-  const int per_spin = NC * O + (NC - 1) * V;
   const double* so[2];
-  const double* sv[2];
-  so[0] = sm; sv[0] = sm + NC * O;
-  so[1] = same ? so[0] : sm + per_spin; sv[1] = same ? sv[0] : sm + per_spin + NC * O;
+  so[0] = sm;
+  so[1] = same ? so[0] : sm + NC * O;
   for (int s = 0; s < (same ? 1 : 2); ++s) {
     const double* po = s ? pO1 : pO0;
-    const double* pv = s ? pV1 : pV0;
-    double* dso = sm + s * per_spin;
-    double* dsv = dso + NC * O;
+    double* dso = sm + s * NC * O;
     for (int k = threadIdx.x; k < NC * O; k += blockDim.x) {
       const int cc = k / O, i = k % O;
       dso[k] = po[cc * compP + gg * nmo + i];
-    }
-    for (int k = threadIdx.x; k < (NC - 1) * V; k += blockDim.x) {
-      const int cc = k / V + 1, a = k % V;
-      dsv[k] = pv[cc * compP + gg * nmo + v0 + a];
     }
   }
   for (int k = threadIdx.x; k < 4 * NC * NC; k += blockDim.x) sk[k] = wfxc[(long)k * ngrid + gg];
@@ -313,7 +303,7 @@ k_xc_uks_w(int g0, int ngrid, int nz, int O, int V, int nmo, int v0, long compP,
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nwave = blockDim.x >> 6;
   double* Ub[2] = {U0 + g * ldU0, U1 + g * ldU1};
-  double* Wb[2] = {W0 ? W0 + g * ldW0 : nullptr, W1 ? W1 + g * ldW1 : nullptr};
+  double* Rb[2] = {R0 ? R0 + g * ldR0 : nullptr, R1 ? R1 + g * ldR1 : nullptr};
   for (int x = wave; x < nz; x += nwave) {
     double acc[2][NC];
 #pragma unroll
@@ -330,29 +320,6 @@ k_xc_uks_w(int g0, int ngrid, int nz, int O, int V, int nmo, int v0, long compP,
         acc[1][c] += a1 * so[1][c * O + i];
       }
     }
-    if (NC > 1) {
-      const double* w0 = Wb[0] + (long)x * V;
-      const double* w1 = Wb[1] + (long)x * V;
-      for (int a0 = lane; a0 < V; a0 += 64 * XW_UNR) {
-        double r0[XW_UNR], r1[XW_UNR];
-#pragma unroll
-        for (int u = 0; u < XW_UNR; ++u) {   // unconditional (clamped) loads: all in flight at once
-          const int a = min(a0 + 64 * u, V - 1);
-          r0[u] = w0[a];
-          r1[u] = w1[a];
-        }
-#pragma unroll
-        for (int u = 0; u < XW_UNR; ++u) {
-          const int a = min(a0 + 64 * u, V - 1);
-          if (a0 + 64 * u >= V) { r0[u] = 0.0; r1[u] = 0.0; }
-#pragma unroll
-          for (int c = 1; c < NC; ++c) {
-            acc[0][c] += r0[u] * sv[0][(c - 1) * V + a];
-            acc[1][c] += r1[u] * sv[1][(c - 1) * V + a];
-          }
-        }
-      }
-    }
     double rho[2][NC];
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -361,6 +328,7 @@ k_xc_uks_w(int g0, int ngrid, int nz, int O, int V, int nmo, int v0, long compP,
         double v = acc[s][c];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (NC > 1 && c > 0) v += Rb[s][3 * x + c - 1];
         rho[s][c] = v;
       }
     double wv[2][NC];
@@ -387,15 +355,16 @@ k_xc_uks_w(int g0, int ngrid, int nz, int O, int V, int nmo, int v0, long compP,
         for (int c = 0; c < NC; ++c) l += wv[s][c] * so[s][c * O + i];
         u[i] = l;
       }
-      if (NC > 1) {
-        double* w = Wb[s] + (long)x * V;
-        for (int a = lane; a < V; a += 64) {
-          double m = 0.0;
+    }
+    if (NC > 1 && lane < 6) {   // all reads of R for this x are done (shuffle-synchronised wave)
+      const int s = lane / 3, c = lane % 3 + 1;
+      double v = 0.0;
 #pragma unroll
-          for (int c = 1; c < NC; ++c) m += wv[s][c] * sv[s][(c - 1) * V + a];
-          w[a] = m;
-        }
-      }
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int y = 1; y < NC; ++y)
+          if (ss == s && y == c) v = wv[ss][y];
+      Rb[s][3 * x + c - 1] = v;
     }
   }
 }
@@ -578,19 +547,17 @@ void xc_uks(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, 
   else
     hipLaunchKernelGGL(k_xc_uks<1>, dim3(blocks), dim3(256), 0, st, G, g0, ngrid, nz, O, nmo, phi0, phi1, wfxc, U);
 }
-void xc_uks_w(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, int V, int nmo, int v0,
-              long compP, const double* pO0, const double* pO1, const double* pV0, const double* pV1,
-              const double* wfxc, double* U0, long ldU0, double* U1, long ldU1,
-              double* W0, long ldW0, double* W1, long ldW1) {
+void xc_uks_w(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
+              const double* pO0, const double* pO1, const double* wfxc, double* U0, long ldU0,
+              double* U1, long ldU1, double* R0, long ldR0, double* R1, long ldR1) {
   const bool same = (pO0 == pO1);
-  const size_t per_spin = (size_t)ncomp * O + (size_t)(ncomp - 1) * V;
-  const size_t lds = (same ? 1 : 2) * per_spin * sizeof(double);
+  const size_t lds = (same ? 1 : 2) * (size_t)ncomp * O * sizeof(double);
   if (ncomp == 4)
-    hipLaunchKernelGGL(k_xc_uks_w<4>, dim3(G), dim3(256), lds, st, g0, ngrid, nz, O, V, nmo, v0, compP,
-                       pO0, pO1, pV0, pV1, wfxc, U0, ldU0, U1, ldU1, W0, ldW0, W1, ldW1);
+    hipLaunchKernelGGL(k_xc_uks_w<4>, dim3(G), dim3(256), lds, st, g0, ngrid, nz, O, nmo, compP,
+                       pO0, pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1);
   else
-    hipLaunchKernelGGL(k_xc_uks_w<1>, dim3(G), dim3(256), lds, st, g0, ngrid, nz, O, V, nmo, v0, compP,
-                       pO0, pO1, pV0, pV1, wfxc, U0, ldU0, U1, ldU1, W0, ldW0, W1, ldW1);
+    hipLaunchKernelGGL(k_xc_uks_w<1>, dim3(G), dim3(256), lds, st, g0, ngrid, nz, O, nmo, compP,
+                       pO0, pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1);
 }
 void xc_sf(hipStream_t st, int G, int g0, int nz, int O, int nmo, const double* phio, const double* fsf, double* U) {
   const long waves = (long)G * nz;
