@@ -83,11 +83,11 @@ def cpu_baseline(args):
                      hyb=args.hyb)
         vind, hdiag = oxtda.gen_tda_operation(mf)
         z = make_trial_vectors(1, hdiag.size)
-        vind(z)                        # warm-up
+        vind(z)                        # warm-up (1 warm-up, median of >= 5)
         ts = []
-        for _ in range(2):
+        for _ in range(5):
             t0 = time.perf_counter(); vind(z); ts.append(time.perf_counter() - t0)
-        times.append(min(ts))
+        times.append(float(np.median(ts)))
         del mf, vind
     (n1, g1), (n2, _), (_, g3) = samples
     a = (times[1] - times[0]) / (n2 - n1)
@@ -96,9 +96,30 @@ def cpu_baseline(args):
     t_vec = t0 + a * naux + b * ngrid
     return dict(value=1.0 / t_vec, unit="matvecs/s", cores=int(cores), kind="port",
                 sample=(f"oracle X-TDA vind (NumPy AO route, DF J/K, GGA) on 1 vector at nao={args.nao}, "
-                        f"(naux, ngrid) in {samples}, min of 2; linear extrapolation to naux={naux}, "
-                        f"ngrid={ngrid}: t_vec = {t_vec:.1f} s"),
-                sample_wall_s=round(time.perf_counter() - t_all, 1))
+                        f"(naux, ngrid) in {samples}, 1 warm-up + median of 5; linear extrapolation to "
+                        f"naux={naux}, ngrid={ngrid}: t_vec = {t_vec:.1f} s"),
+                host=_host_info(), sample_wall_s=round(time.perf_counter() - t_all, 1))
+
+
+def _host_info():
+    """CPU model and BLAS build of the host timing the CPU baseline."""
+    info = {}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["cpu"] = line.split(":", 1)[1].strip()
+                    break
+        info["host_cpus"] = os.cpu_count()
+    except Exception:
+        pass
+    try:
+        from threadpoolctl import threadpool_info
+        info["blas"] = [f"{i.get('internal_api')} {i.get('version')} threads={i.get('num_threads')}"
+                        for i in threadpool_info()]
+    except Exception:
+        pass
+    return info
 
 
 def load_traffic(tag_name):

@@ -162,19 +162,28 @@ dgemm_kernel(GemmParams p) {
     }
   }
   a_row0 = (unsigned)(rowoff(min(m0 + a_fix, p.M - 1)) * 8);
-  // mode 2: this thread's fixed virtual index a (column % 16) and per-element xg
-  const int a_gen = a_blk * 16 + (b_var & 15);
-  const bool a_ok = a_gen < p.fz.V;
-  const int a_cl = a_ok ? a_gen : p.fz.V - 1;
-  if (MODE == 2) {
+  // mode 2 staging map (BK = 32 k rows x 128 columns = 8 xg x 16 a): thread ->
+  // k row g2 = 4 wave + (tid >> 2 & 3), xg pair 2 p2 + {0,1} (p2 = tid >> 4 & 3), a quad
+  // 4 aq + {0..3} (aq = tid & 3): 6 rho + 12 gradient loads for 8 elements, each
+  // wave-load touching 4 grid rows, and the LDS stores of a 16-lane group land on
+  // 16 distinct bank pairs (4 rows x 4 quads, pitch 33).
+  const int g2 = (tid >> 6) * 4 + ((tid >> 2) & 3), p2 = (tid >> 4) & 3, aq2 = tid & 3;
+  int xg2[2], a2[4];
+  bool ok2[2][4];
 #pragma unroll
-    for (int e = 0; e < B_ELEMS; ++e) {
-      const int xg = xg_blk * 8 + (b_var + e * B_STEP) / 16;
-      boff[e] = (unsigned)((xg < p.fz.nx ? xg : p.fz.nx - 1) * 3);   // rho offset (doubles)
-    }
-  }
-  double bw[MODE == 2 ? 3 : 1];                    // mode 2: w_c[g][a] of the staged k row
-  double br[MODE == 2 ? B_ELEMS : 1][3];           // mode 2: rho[g][xg_e][c]
+  for (int x = 0; x < 2; ++x) xg2[x] = xg_blk * 8 + 2 * p2 + x;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) a2[u] = a_blk * 16 + 4 * aq2 + u;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ok2[x][u] = xg2[x] < p.fz.nx && a2[u] < p.fz.V;
+#pragma unroll
+  for (int x = 0; x < 2; ++x) xg2[x] = xg2[x] < p.fz.nx ? xg2[x] : p.fz.nx - 1;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) a2[u] = a2[u] < p.fz.V ? a2[u] : p.fz.V - 1;
+  double bw[MODE == 2 ? 4 : 1][3];                 // mode 2: w_c[g][a_u]
+  double br[MODE == 2 ? 2 : 1][3];                 // mode 2: rho[g][xg_x][c]
   b_row0 = (unsigned)((min(n0 + b_fix, p.N - 1) - n0) * 8);
 
   double ra[A_ELEMS], rb[B_ELEMS];
@@ -196,13 +205,15 @@ dgemm_kernel(GemmParams p) {
     }
     if constexpr (MODE == 2) {
       // generated operand: raw inputs of k row g (clamped to the tile's first row past K)
-      const long g = k0 + (b_fix < kv ? b_fix : 0);
+      const long g = k0 + (g2 < kv ? g2 : 0);
 #pragma unroll
-      for (int c = 0; c < 3; ++c) bw[c] = p.fz.w[c * p.fz.wc + g * p.fz.wg + a_cl];
+      for (int x = 0; x < 2; ++x)
 #pragma unroll
-      for (int e = 0; e < B_ELEMS; ++e)
+        for (int c = 0; c < 3; ++c) br[x][c] = p.fz.rho[g * p.fz.rg + 3 * xg2[x] + c];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) br[e][c] = p.fz.rho[g * p.fz.rg + boff[e] + c];
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) bw[u][c] = p.fz.w[c * p.fz.wc + g * p.fz.wg + a2[u]];
     } else {
 #pragma unroll
       for (int e = 0; e < B_ELEMS; ++e) {
@@ -221,19 +232,22 @@ dgemm_kernel(GemmParams p) {
       if (A_KC) { mm = a_var + e * A_STEP; kk = a_fix; } else { kk = a_var + e * A_STEP; mm = a_fix; }
       smem[buf * STAGE + mm * LDP + kk] = ra[e];
     }
+    if constexpr (MODE == 2) {
 #pragma unroll
-    for (int e = 0; e < B_ELEMS; ++e) {
-      int nn, kk;
-      if (B_KC) { nn = b_var + e * B_STEP; kk = b_fix; } else { kk = b_var + e * B_STEP; nn = b_fix; }
-      double v;
-      if constexpr (MODE == 2) {
-        const int xg = xg_blk * 8 + nn / 16;
-        v = br[e][0] * bw[0] + br[e][1] * bw[1] + br[e][2] * bw[2];
-        v = (a_ok && xg < p.fz.nx && kk < kv) ? v : 0.0;
-      } else {
-        v = (kk < kv) ? rb[e] : 0.0;
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int nn = (2 * p2 + x) * 16 + 4 * aq2 + u;
+          const double v = br[x][0] * bw[u][0] + br[x][1] * bw[u][1] + br[x][2] * bw[u][2];
+          smem[buf * STAGE + BM * LDP + nn * LDP + g2] = (ok2[x][u] && g2 < kv) ? v : 0.0;
+        }
+    } else {
+#pragma unroll
+      for (int e = 0; e < B_ELEMS; ++e) {
+        int nn, kk;
+        if (B_KC) { nn = b_var + e * B_STEP; kk = b_fix; } else { kk = b_var + e * B_STEP; nn = b_fix; }
+        smem[buf * STAGE + BM * LDP + nn * LDP + kk] = (kk < kv) ? rb[e] : 0.0;
       }
-      smem[buf * STAGE + BM * LDP + nn * LDP + kk] = v;
     }
   };
   // MFMA sub-tiles of this wave that hold any row < M / col < N; a wave whose
@@ -334,34 +348,38 @@ dgemm_kernel(GemmParams p) {
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int c = 0; c < 3; ++c) racc[j][c] = 0.0;
-    auto rho_epilogue = [&](int r) XT_INLINE {
+    // gradient weights w_c[g][a] of this lane's column sub-tile j, a = 16 r + q + 4 t
+    auto load_w = [&](int r, int j, double (&w)[3][4]) XT_INLINE {
+      const int g = min(n0 + wn * WN + j * 16 + r16, p.N - 1);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int g = min(n0 + wn * WN + j * 16 + r16, p.N - 1);
-        double w[3][4];
+      for (int t = 0; t < 4; ++t) {
+        const int a = 16 * r + q + 4 * t;
+        const int acl = a < p.fz.V ? a : p.fz.V - 1;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int a = 16 * r + q + 4 * t;
-          const bool ok = a < p.fz.V;
-          const int acl = ok ? a : p.fz.V - 1;
+        for (int c = 0; c < 3; ++c) w[c][t] = p.fz.w[c * p.fz.wc + (long)g * p.fz.wg + acl];
+      }
+    };
+    // contract sub-tile column j of the accumulators with its weights, reduce
+    // over the 16 a of each row sub-tile (4 in-lane + 4 lanes q), clear it
+    auto reduce_j = [&](int r, int j, const double (&w)[3][4]) XT_INLINE {
+      double wz[3][4];
 #pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const double wv = p.fz.w[c * p.fz.wc + (long)g * p.fz.wg + acl];
-            w[c][t] = ok ? wv : 0.0;
-          }
+      for (int t = 0; t < 4; ++t) {
+        const bool ok = 16 * r + q + 4 * t < p.fz.V;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) wz[c][t] = ok ? w[c][t] : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          double sv = acc[i][j][0] * wz[c][0] + acc[i][j][1] * wz[c][1] + acc[i][j][2] * wz[c][2] +
+                      acc[i][j][3] * wz[c][3];
+          sv += __shfl_xor(sv, 16);
+          sv += __shfl_xor(sv, 32);
+          if (q == i) racc[j][c] += sv;
         }
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            double sv = acc[i][j][0] * w[c][0] + acc[i][j][1] * w[c][1] + acc[i][j][2] * w[c][2] +
-                        acc[i][j][3] * w[c][3];
-            sv += __shfl_xor(sv, 16);
-            sv += __shfl_xor(sv, 32);
-            if (q == i) racc[j][c] += sv;
-          }
-          acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
-        }
+        acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
       }
     };
     auto run1 = [&](auto MN_EDGE) XT_INLINE {
@@ -384,7 +402,12 @@ dgemm_kernel(GemmParams p) {
         store_tile(buf ^ 1, kv);
         __syncthreads();
         buf ^= 1;
-        rho_epilogue(r);
+        // (prefetching w behind the last K-tile costs 30 VGPRs and measured slower)
+        double w[3][4];
+        load_w(r, 0, w);
+        reduce_j(r, 0, w);
+        load_w(r, 1, w);
+        reduce_j(r, 1, w);
       }
     };
     if (nkt > 0) {
