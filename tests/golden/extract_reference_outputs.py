@@ -1,0 +1,95 @@
+"""Extract the reference's own stored results into ``reference_outputs.json``.
+
+Run in the build container (``/root/reference`` exists only there):
+
+    python tests/golden/extract_reference_outputs.py
+
+Sources (PySCF 2.12.1 / libxc 7.0.0 runs recorded by the reference authors):
+
+* ``example/XSF_TDA.ipynb`` cell 1  -- HF molecule (F 0 0 0; H 0 0 1.0 A), 6-31G,
+  spin 2, C2v, ``irrep_nelec {'A1':(4,2),'B1':(1,1),'B2':(1,1)}``, ROKS/BHandHLYP:
+  nuclear repulsion, cond(S), per-atom pruned grid sizes, total grid count,
+  converged SCF energy, final Roothaan orbital energies.
+* cell 2 -- XSF-TDA (ALDA0, SA=3, remove=True) 10 roots in eV.
+* cell 5 / 6 -- the same molecule with UKS: SCF energy, USF-TDA (XSF_TDA on a
+  UKS mf: SA=0, no OO compression) 10 roots in eV and the Delta<S^2> list.
+* ``example/spin up.ipynb`` cell 1 -- H 0 0 0; F 0 0 1.0 A ROKS/BHandHLYP aufbau
+  triplet SCF energy.
+
+Only numbers are extracted (the fixture is data); no reference code is copied.
+"""
+from __future__ import annotations
+
+import json
+import os
+import re
+
+import numpy as np
+
+REF = "/root/reference/example"
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_outputs.json")
+
+
+def _outputs(cell):
+    texts = []
+    for o in cell.get("outputs", []):
+        t = "".join(o.get("text", ""))
+        if not t and "data" in o:
+            t = "".join(o["data"].get("text/plain", ""))
+        texts.append(t)
+    return texts
+
+
+def _floats(s):
+    return [float(x) for x in re.findall(r"[-+]?\d+\.\d+(?:e[-+]?\d+)?", s)]
+
+
+def _bracket_after(text, key):
+    i = text.index(key)
+    j = text.index("[", i)
+    k = text.index("]", j)
+    return text[j + 1:k]
+
+
+def main():
+    nb = json.load(open(os.path.join(REF, "XSF_TDA.ipynb")))
+    cells = nb["cells"]
+    out = {"source": "reference example notebooks (PySCF 2.12.1, libxc 7.0.0)"}
+
+    log = "\n".join(_outputs(cells[1]))
+    out["hf_631g_nuclear_repulsion"] = float(re.search(r"nuclear repulsion = ([-\d.]+)", log).group(1))
+    out["hf_631g_cond_S"] = float(re.search(r"cond\(S\) = ([-\d.]+)", log).group(1))
+    out["hf_631g_grid_ang_F"] = [int(x) for x in _bracket_after(log, "atom F rad-grids").split()]
+    out["hf_631g_grid_ang_H"] = [int(x) for x in _bracket_after(log, "atom H rad-grids").split()]
+    out["hf_631g_tot_grids_padded"] = int(re.search(r"tot grids = (\d+)", log).group(1))
+    out["hf_631g_padding"] = int(re.search(r"Padding (\d+) grids", log).group(1))
+    out["roks_bhandhlyp_e_tot"] = float(re.search(r"converged SCF energy = ([-\d.]+)", log).group(1))
+    roothaan = log.rsplit("Roothaan mo_energy =", 1)[1]
+    out["roks_bhandhlyp_mo_energy_last_cycle"] = _floats(roothaan[:roothaan.index("]")])
+
+    xsf = "\n".join(_outputs(cells[2]))
+    out["xsf_roks_alda0_fglobal"] = float(re.search(r"fglobal ([-\d.]+)", xsf).group(1))
+    # the eigenvalue list is the bracket after the "Converged [True ...]" line
+    out["xsf_roks_alda0_ev"] = _floats(xsf[xsf.index("]", xsf.index("Converged")) + 1:].split("]")[0])
+    log5 = "\n".join(_outputs(cells[5]))
+    out["uks_bhandhlyp_e_tot"] = float(_floats(_outputs(cells[5])[-1])[0])
+    s2 = re.findall(r"multiplicity <S\^2> = ([\d.]+)", log5)
+    out["uks_bhandhlyp_s2_last_printed"] = float(s2[-1])
+    usf = "\n".join(_outputs(cells[6]))
+    out["usf_uks_alda0_ev"] = _floats(usf[usf.index("]", usf.index("Converged")) + 1:].split("]")[0])
+    tail = _outputs(cells[6])[-1]
+    out["usf_uks_alda0_delta_s2"] = _floats(tail[:tail.index("]")])
+
+    nb2 = json.load(open(os.path.join(REF, "spin up.ipynb")))
+    up = "\n".join(_outputs(nb2["cells"][1]))
+    out["roks_aufbau_hf_e_tot"] = float(re.search(r"converged SCF energy = ([-\d.]+)", up).group(1))
+
+    assert len(out["xsf_roks_alda0_ev"]) == 10 and len(out["usf_uks_alda0_ev"]) == 10
+    assert len(out["hf_631g_grid_ang_F"]) == 75 and len(out["hf_631g_grid_ang_H"]) == 50
+    json.dump(out, open(OUT, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    np.set_printoptions(precision=12)
+    main()

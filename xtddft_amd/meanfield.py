@@ -177,7 +177,10 @@ class MeanField:
         return self.omega, self.alpha, self.hyb
 
     def spin_square(self):
-        """<S^2> and 2S+1 of a pure spin state (ROKS), as PySCF returns them."""
+        """<S^2> and 2S+1 as PySCF returns them: the pure-state value for ROKS; for a
+        UKS determinant the SCF driver's value when it supplied one."""
+        if "spin_square" in self.extra:
+            return self.extra["spin_square"]
         s = 0.5 * self.mol.spin
         return s * (s + 1), 2 * s + 1
 

@@ -1,0 +1,311 @@
+"""``Mole``: atoms + spherical Gaussian basis, the ``gto.M(...)`` the reference's
+drivers start from (``example/XSF_TDA.ipynb`` cell 1, ``XTDA.py:1486-1556``).
+
+Conventions follow PySCF/libcint so that AO-basis quantities are directly
+comparable with the reference:
+
+* coordinates in Bohr, ``BOHR = 0.52917721092`` Angstrom (PySCF ``param.BOHR``);
+* spherical AOs, shell by shell in input order; p shells ordered (px, py, pz),
+  d shells (xy, yz, z^2, xz, x^2-y^2);
+* primitive coefficients scaled by the radial norm of r^l exp(-a r^2) and each
+  AO normalised to one (PySCF ``NORMALIZE_GTO``), so ``diag(S) = 1``.
+
+Point-group symmetry is supported for the case the reference examples use:
+linear or planar molecules whose symmetry planes are the xz / yz planes
+(C2v with the z axis as C2; ``Coov`` is run in its C2v subgroup, as PySCF does,
+``example/XSF_TDA.ipynb``: "point group symmetry = Coov, use subgroup C2v").
+Each AO then belongs to one irrep (``ao_irreps``).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Sequence
+
+import numpy as np
+
+from . import basis as _basis
+from .ints import ShellPair, cart_comps, eri_quartet
+
+BOHR = 0.52917721092
+
+ELEMENTS = ["X", "H", "He", "Li", "Be", "B", "C", "N", "O", "F", "Ne", "Na", "Mg", "Al", "Si",
+            "P", "S", "Cl", "Ar", "K", "Ca", "Sc", "Ti", "V", "Cr", "Mn", "Fe", "Co", "Ni", "Cu",
+            "Zn", "Ga", "Ge", "As", "Se", "Br", "Kr"]
+CHARGE = {s: i for i, s in enumerate(ELEMENTS)}
+
+C2V_IRREPS = ("A1", "A2", "B1", "B2")     # PySCF order; B1 ~ x, B2 ~ y
+
+
+def _sph_transform(l: int) -> np.ndarray:
+    """(n_sph, n_cart) un-normalised real solid harmonics in libcint order."""
+    if l == 0:
+        return np.ones((1, 1))
+    if l == 1:
+        return np.eye(3)
+    if l == 2:
+        # cart order: xx xy xz yy yz zz
+        return np.array([
+            [0, 1, 0, 0, 0, 0],          # xy
+            [0, 0, 0, 0, 1, 0],          # yz
+            [-1, 0, 0, -1, 0, 2],        # 2zz - xx - yy
+            [0, 0, 1, 0, 0, 0],          # xz
+            [1, 0, 0, -1, 0, 0],         # xx - yy
+        ], dtype=np.float64)
+    raise NotImplementedError("shells with l > 2 are not supported")
+
+
+def gto_norm(l: int, a: np.ndarray) -> np.ndarray:
+    """Radial norm of r^l exp(-a r^2) (PySCF gto.gto_norm)."""
+    return np.sqrt(2.0 * (2.0 * a) ** (l + 1.5) / math.gamma(l + 1.5))
+
+
+@dataclass
+class Shell:
+    atom: int
+    l: int
+    center: np.ndarray
+    exps: np.ndarray
+    coefs: np.ndarray          # primitive coefficients x radial norms (one contraction)
+
+    @property
+    def ncart(self):
+        return (self.l + 1) * (self.l + 2) // 2
+
+    @property
+    def nsph(self):
+        return 2 * self.l + 1
+
+
+def _parse_atoms(atom) -> List[tuple]:
+    if isinstance(atom, str):
+        items = []
+        for line in atom.replace(";", "\n").splitlines():
+            f = line.split()
+            if not f:
+                continue
+            items.append((f[0], tuple(float(x) for x in f[1:4])))
+        return items
+    return [(a[0], tuple(float(x) for x in a[1])) for a in atom]
+
+
+class Mole:
+    """Minimal ``gto.Mole``: geometry, basis, electron count, integrals."""
+
+    def __init__(self, atom, basis="6-31G", charge: int = 0, spin: int = 0,
+                 unit: str = "Angstrom", symmetry=False, verbose: int = 0):
+        self.atom = atom
+        self.basis = basis
+        self.charge = int(charge)
+        self.spin = int(spin)
+        self.unit = unit
+        self.verbose = verbose
+        atoms = _parse_atoms(atom)
+        scale = 1.0 / BOHR if unit.lower().startswith("a") else 1.0
+        self.elements = [a[0].capitalize() for a in atoms]
+        self._coords = np.array([a[1] for a in atoms], dtype=np.float64) * scale
+        self._charges = np.array([CHARGE[e] for e in self.elements], dtype=np.float64)
+        self.nelectron = int(round(self._charges.sum())) - self.charge
+        if (self.nelectron + self.spin) % 2:
+            raise ValueError(f"electron number {self.nelectron} and spin {self.spin} are inconsistent")
+        self.shells: List[Shell] = []
+        for ia, el in enumerate(self.elements):
+            for sh in _basis.load(basis, el):
+                l = int(sh[0])
+                prim = np.array(sh[1:], dtype=np.float64)
+                exps = prim[:, 0]
+                for ic in range(1, prim.shape[1]):
+                    c = prim[:, ic] * gto_norm(l, exps)
+                    self.shells.append(Shell(ia, l, self._coords[ia].copy(), exps.copy(), c))
+        self.ao_loc = np.cumsum([0] + [s.nsph for s in self.shells])
+        self._nao = int(self.ao_loc[-1])
+        self.symmetry = self._check_symmetry(symmetry)
+        self._norm = None
+        self._norm = 1.0 / np.sqrt(np.diag(self._intor_raw("ovlp")))
+
+    # -------------------------------------------------------------- basics
+    def nao_nr(self) -> int:
+        return self._nao
+
+    @property
+    def nao(self) -> int:
+        return self._nao
+
+    @property
+    def natm(self) -> int:
+        return len(self.elements)
+
+    @property
+    def nelec(self):
+        return ((self.nelectron + self.spin) // 2, (self.nelectron - self.spin) // 2)
+
+    def atom_coords(self) -> np.ndarray:
+        return self._coords.copy()
+
+    def atom_charges(self) -> np.ndarray:
+        return self._charges.astype(np.int64)
+
+    def energy_nuc(self) -> float:
+        e = 0.0
+        for i in range(self.natm):
+            for j in range(i):
+                e += self._charges[i] * self._charges[j] / np.linalg.norm(self._coords[i] - self._coords[j])
+        return e
+
+    def ao_atom(self) -> np.ndarray:
+        out = np.empty(self._nao, dtype=np.int64)
+        for s, p0, p1 in zip(self.shells, self.ao_loc[:-1], self.ao_loc[1:]):
+            out[p0:p1] = s.atom
+        return out
+
+    # ------------------------------------------------------------ symmetry
+    def _check_symmetry(self, symmetry):
+        if not symmetry:
+            return None
+        group = str(symmetry)
+        if group is True or group.lower() in ("true", "c2v", "coov"):
+            xy = self._coords[:, :2]
+            if np.abs(xy).max() > 1e-8:
+                raise NotImplementedError("symmetry is supported for molecules on the z axis "
+                                          "(C2v / Coov run in C2v)")
+            return "C2v"
+        raise NotImplementedError(f"point group {symmetry!r} not supported (C2v / Coov only)")
+
+    def ao_irreps(self) -> np.ndarray:
+        """Irrep index (into C2V_IRREPS) of every AO under C2v (z = C2 axis)."""
+        if self.symmetry is None:
+            raise ValueError("mol.symmetry is off")
+        out = np.empty(self._nao, dtype=np.int64)
+        for s, p0 in zip(self.shells, self.ao_loc[:-1]):
+            T = _sph_transform(s.l)
+            comps = cart_comps(s.l)
+            for m in range(s.nsph):
+                nz = [comps[c] for c in range(len(comps)) if abs(T[m, c]) > 0]
+                px = {c[0] % 2 for c in nz}
+                py = {c[1] % 2 for c in nz}
+                assert len(px) == 1 and len(py) == 1
+                odd_x, odd_y = px.pop(), py.pop()
+                out[p0 + m] = {(0, 0): 0, (1, 1): 1, (1, 0): 2, (0, 1): 3}[(odd_x, odd_y)]
+        return out
+
+    # ----------------------------------------------------------- integrals
+    def _intor_raw(self, kind, origin=(0.0, 0.0, 0.0)):
+        n = self._nao
+        if kind == "r":
+            out = np.zeros((3, n, n))
+        else:
+            out = np.zeros((n, n))
+        sh = self.shells
+        for i, si in enumerate(sh):
+            Ti = _sph_transform(si.l)
+            for j in range(i + 1):
+                sj = sh[j]
+                Tj = _sph_transform(sj.l)
+                pair = ShellPair(si, sj, kin=(kind == "kin"))
+                if kind == "ovlp":
+                    blk = pair.overlap()
+                elif kind == "kin":
+                    blk = pair.kinetic()
+                elif kind == "nuc":
+                    blk = pair.nuclear(self._charges, self._coords)
+                elif kind == "r":
+                    blk = pair.multipole1(np.asarray(origin, dtype=np.float64))
+                else:
+                    raise KeyError(kind)
+                blk = Ti @ blk @ Tj.T if kind != "r" else np.einsum('mi,dij,nj->dmn', Ti, blk, Tj)
+                a0, a1 = self.ao_loc[i], self.ao_loc[i + 1]
+                b0, b1 = self.ao_loc[j], self.ao_loc[j + 1]
+                if kind == "r":
+                    out[:, a0:a1, b0:b1] = blk
+                    out[:, b0:b1, a0:a1] = blk.transpose(0, 2, 1)
+                else:
+                    out[a0:a1, b0:b1] = blk
+                    out[b0:b1, a0:a1] = blk.T
+        if self._norm is not None:
+            nrm = self._norm
+            out = out * (nrm[:, None] * nrm[None, :])
+        return out
+
+    def intor(self, name: str, origin=(0.0, 0.0, 0.0)):
+        """PySCF names: int1e_ovlp, int1e_kin, int1e_nuc, int1e_r, int2e."""
+        key = name.replace("_sph", "")
+        if key == "int1e_ovlp":
+            return self._intor_raw("ovlp")
+        if key == "int1e_kin":
+            return self._intor_raw("kin")
+        if key == "int1e_nuc":
+            return self._intor_raw("nuc")
+        if key == "int1e_r":
+            return self._intor_raw("r", origin)
+        if key == "int2e":
+            return self.eri_full()
+        raise KeyError(name)
+
+    def eri_full(self) -> np.ndarray:
+        """(mu nu|la si) over normalised spherical AOs, all 8 symmetry copies filled."""
+        n = self._nao
+        sh = self.shells
+        nsh = len(sh)
+        T = [_sph_transform(s.l) for s in sh]
+        pairs = {}
+        for i in range(nsh):
+            for j in range(i + 1):
+                pairs[(i, j)] = ShellPair(sh[i], sh[j])
+        eri = np.zeros((n, n, n, n))
+        keys = list(pairs)
+        for ij, (i, j) in enumerate(keys):
+            bra = pairs[(i, j)]
+            for (k, l) in keys[:ij + 1]:
+                ket = pairs[(k, l)]
+                blk = eri_quartet(bra, ket)
+                blk = np.einsum('ai,bj,ijkl,ck,dl->abcd', T[i], T[j], blk, T[k], T[l], optimize=True)
+                a = slice(self.ao_loc[i], self.ao_loc[i + 1])
+                b = slice(self.ao_loc[j], self.ao_loc[j + 1])
+                c = slice(self.ao_loc[k], self.ao_loc[k + 1])
+                d = slice(self.ao_loc[l], self.ao_loc[l + 1])
+                for (x, y, bx) in ((a, b, blk), (b, a, blk.transpose(1, 0, 2, 3))):
+                    for (z, w, bz) in ((c, d, bx), (d, c, bx.transpose(0, 1, 3, 2))):
+                        eri[x, y, z, w] = bz
+                        eri[z, w, x, y] = bz.transpose(2, 3, 0, 1)
+        nrm = self._norm
+        eri *= (nrm[:, None, None, None] * nrm[None, :, None, None]
+                * nrm[None, None, :, None] * nrm[None, None, None, :])
+        return eri
+
+    # ----------------------------------------------------- AO on the grid
+    def eval_ao(self, coords: np.ndarray, deriv: int = 0) -> np.ndarray:
+        """AO values (deriv 0: (ngrid, nao)) or values + gradients (deriv 1: (4, ngrid, nao))."""
+        coords = np.asarray(coords, dtype=np.float64)
+        ng = coords.shape[0]
+        ncomp = 4 if deriv else 1
+        out = np.empty((ncomp, ng, self._nao))
+        for s, p0, p1 in zip(self.shells, self.ao_loc[:-1], self.ao_loc[1:]):
+            d = coords - s.center
+            r2 = np.einsum('gx,gx->g', d, d)
+            ex = np.exp(-np.outer(r2, s.exps))            # (ng, nprim)
+            g0 = ex @ s.coefs
+            comps = cart_comps(s.l)
+            cart = np.empty((ncomp, ng, len(comps)))
+            if deriv:
+                g1 = ex @ (-2.0 * s.exps * s.coefs)         # d/d(r^2) part: grad = g1 * d
+            for c, (ix, iy, iz) in enumerate(comps):
+                poly = d[:, 0] ** ix * d[:, 1] ** iy * d[:, 2] ** iz
+                cart[0, :, c] = poly * g0
+                if deriv:
+                    for k, e in enumerate((ix, iy, iz)):
+                        if e > 0:
+                            pe = list((ix, iy, iz))
+                            pe[k] -= 1
+                            dpoly = e * d[:, 0] ** pe[0] * d[:, 1] ** pe[1] * d[:, 2] ** pe[2]
+                        else:
+                            dpoly = 0.0
+                        cart[1 + k, :, c] = dpoly * g0 + poly * d[:, k] * g1
+            T = _sph_transform(s.l)
+            out[:, :, p0:p1] = np.einsum('xgc,mc->xgm', cart, T) * self._norm[p0:p1]
+        return out if deriv else out[0]
+
+
+def M(atom, basis="6-31G", charge=0, spin=0, unit="Angstrom", symmetry=False, verbose=0) -> Mole:
+    """``gto.M`` equivalent."""
+    return Mole(atom, basis=basis, charge=charge, spin=spin, unit=unit, symmetry=symmetry,
+                verbose=verbose)

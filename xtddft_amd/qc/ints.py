@@ -1,0 +1,256 @@
+"""Gaussian integrals by the McMurchie-Davidson scheme (replaces libcint for the
+hot path's inputs: ``int1e_ovlp``, ``int1e_kin``, ``int1e_nuc``, ``int1e_r``,
+``int2e`` as PySCF's ``mol.intor`` returns them, XTDA.py:120,848,869).
+
+Cartesian primitives x^i y^j z^k exp(-a r^2) are expanded in Hermite Gaussians
+(E coefficients, one recursion per Cartesian direction); Coulomb-type
+integrals use the Hermite integrals R_tuv built by the standard downward
+recursion from Boys functions.  Everything is vectorised over primitive pairs
+(bra) x primitive pairs (ket); the Python loops run over shells only.
+The spherical transform and AO normalisation are applied by ``gto.Mole``.
+"""
+from __future__ import annotations
+
+from functools import lru_cache
+
+import numpy as np
+from scipy.special import gamma as _gamma, gammainc as _gammainc
+
+
+# --------------------------------------------------------------------------- Boys
+def boys(nmax: int, t: np.ndarray) -> np.ndarray:
+    """F_n(T) for n = 0..nmax (shape (nmax+1,) + T.shape), ~1e-15 relative.
+
+    F_nmax from the positive series e^-T sum_k (2T)^k / ((2n+1)(2n+3)...(2n+2k+1))
+    for T < 12 and from the incomplete gamma function above; lower orders by the
+    stable downward recursion F_n = (2T F_{n+1} + e^-T) / (2n+1).
+    """
+    t = np.asarray(t, dtype=np.float64)
+    out = np.empty((nmax + 1,) + t.shape)
+    et = np.exp(-t)
+    small = t < 12.0
+    fn = np.empty(t.shape)
+    if np.any(small):
+        ts = t[small]
+        term = np.full(ts.shape, 1.0 / (2 * nmax + 1))
+        acc = term.copy()
+        for k in range(1, 80):
+            term = term * (2.0 * ts) / (2 * nmax + 2 * k + 1)
+            acc += term
+        fn[small] = et[small] * acc
+    if np.any(~small):
+        tl = t[~small]
+        a = nmax + 0.5
+        fn[~small] = _gamma(a) * _gammainc(a, tl) / (2.0 * tl ** a)
+    out[nmax] = fn
+    for n in range(nmax - 1, -1, -1):
+        out[n] = (2.0 * t * out[n + 1] + et) / (2 * n + 1)
+    return out
+
+
+# --------------------------------------------------------------- index helpers
+@lru_cache(maxsize=None)
+def cart_comps(l: int):
+    """Cartesian components of a shell in PySCF/libcint order (xx, xy, xz, yy, yz, zz ...)."""
+    out = []
+    for ix in range(l, -1, -1):
+        for iy in range(l - ix, -1, -1):
+            out.append((ix, iy, l - ix - iy))
+    return tuple(out)
+
+
+@lru_cache(maxsize=None)
+def hermite_index(L: int):
+    """All (t,u,v) with t+u+v <= L and a dict (t,u,v) -> position."""
+    tuv = [(t, u, v) for n in range(L + 1) for t in range(n, -1, -1)
+           for u in range(n - t, -1, -1) for v in [n - t - u]]
+    return tuple(tuv), {k: i for i, k in enumerate(tuv)}
+
+
+@lru_cache(maxsize=None)
+def _sum_table(lab: int, lcd: int):
+    """idx[i_ab, i_cd] of (t+tau, u+nu, v+phi) in hermite_index(lab+lcd), and (-1)^(tau+nu+phi)."""
+    tab, _ = hermite_index(lab)
+    tcd, _ = hermite_index(lcd)
+    _, pos = hermite_index(lab + lcd)
+    idx = np.empty((len(tab), len(tcd)), dtype=np.int64)
+    for i, (t, u, v) in enumerate(tab):
+        for j, (a, b, c) in enumerate(tcd):
+            idx[i, j] = pos[(t + a, u + b, v + c)]
+    sign = np.array([(-1.0) ** (a + b + c) for (a, b, c) in tcd])
+    return idx, sign
+
+
+# ------------------------------------------------------------ E coefficients
+def hermite_e(la: int, lb: int, a: np.ndarray, b: np.ndarray, xab: float) -> np.ndarray:
+    """E^{ij}_t for one Cartesian direction: shape (la+1, lb+1, la+lb+1) + a.shape.
+
+    a, b broadcast to the primitive-pair shape; xab = A_x - B_x.
+    """
+    p = a + b
+    xpa = -b * xab / p
+    xpb = a * xab / p
+    oo2p = 0.5 / p
+    tmax = la + lb
+    E = np.zeros((la + 1, lb + 1, tmax + 1) + p.shape)
+    E[0, 0, 0] = np.exp(-(a * b / p) * xab * xab)
+    for i in range(la + 1):
+        for j in range(lb + 1):
+            if i == 0 and j == 0:
+                continue
+            if i > 0:
+                src, x = E[i - 1, j], xpa
+                top = i - 1 + j
+            else:
+                src, x = E[i, j - 1], xpb
+                top = i + j - 1
+            for t in range(i + j + 1):
+                v = x * src[t] if t <= top else 0.0
+                if t > 0:
+                    v = v + oo2p * src[t - 1]
+                if t + 1 <= top:
+                    v = v + (t + 1) * src[t + 1]
+                E[i, j, t] = v
+    return E
+
+
+# ------------------------------------------------------------ R integrals
+def hermite_r(L: int, alpha: np.ndarray, X: np.ndarray, Y: np.ndarray, Z: np.ndarray) -> np.ndarray:
+    """R^0_{tuv}(alpha, X, Y, Z) for every (t,u,v) of hermite_index(L): (ntuv,) + X.shape."""
+    F = boys(L, alpha * (X * X + Y * Y + Z * Z))
+    m2a = -2.0 * alpha
+    prev = {(0, 0, 0): m2a ** L * F[L]}
+    for n in range(L - 1, -1, -1):
+        cur = {(0, 0, 0): m2a ** n * F[n]}
+        for tot in range(1, L - n + 1):
+            for t in range(tot, -1, -1):
+                for u in range(tot - t, -1, -1):
+                    v = tot - t - u
+                    if t > 0:
+                        val = X * prev[(t - 1, u, v)]
+                        if t > 1:
+                            val = val + (t - 1) * prev[(t - 2, u, v)]
+                    elif u > 0:
+                        val = Y * prev[(0, u - 1, v)]
+                        if u > 1:
+                            val = val + (u - 1) * prev[(0, u - 2, v)]
+                    else:
+                        val = Z * prev[(0, 0, v - 1)]
+                        if v > 1:
+                            val = val + (v - 1) * prev[(0, 0, v - 2)]
+                    cur[(t, u, v)] = val
+        prev = cur
+    tuv, _ = hermite_index(L)
+    return np.stack([prev[k] for k in tuv])
+
+
+# ------------------------------------------------------------ shell pairs
+class ShellPair:
+    """Primitive-pair data of two contracted Cartesian shells (A, B).
+
+    Eab[ca, cb, i_tuv, q]  Hermite expansion coefficients with contraction
+                           coefficients folded in (q runs over na*nb pairs),
+    p[q], P[q, 3]          combined exponents / centres.
+    """
+
+    def __init__(self, sa, sb, kin: bool = False):
+        self.sa, self.sb = sa, sb
+        la, lb = sa.l, sb.l
+        a = sa.exps[:, None]
+        b = sb.exps[None, :]
+        AB = sa.center - sb.center
+        ext = 2 if kin else 0
+        self.E = [hermite_e(la, lb + ext, a, b, AB[d]) for d in range(3)]
+        p = a + b
+        self.p = p.ravel()
+        self.P = ((a[..., None] * sa.center + b[..., None] * sb.center) / p[..., None]).reshape(-1, 3)
+        cc = (sa.coefs[:, None] * sb.coefs[None, :]).ravel()
+        self.cc = cc
+        L = la + lb
+        tuv, _ = hermite_index(L)
+        ca, cb = cart_comps(la), cart_comps(lb)
+        Eab = np.zeros((len(ca), len(cb), len(tuv), self.p.size))
+        Ex, Ey, Ez = (e.reshape(e.shape[:3] + (-1,)) for e in self.E)
+        for i, (ax, ay, az) in enumerate(ca):
+            for j, (bx, by, bz) in enumerate(cb):
+                for k, (t, u, v) in enumerate(tuv):
+                    if t > ax + bx or u > ay + by or v > az + bz:
+                        continue
+                    Eab[i, j, k] = Ex[ax, bx, t] * Ey[ay, by, u] * Ez[az, bz, v] * cc
+        self.Eab = Eab
+        self.L = L
+
+    # 1D overlap table S[i, j] over primitive pairs, with the sqrt(pi/p) factor
+    def _s1d(self, d):
+        e = self.E[d].reshape(self.E[d].shape[:3] + (-1,))
+        return e[:, :, 0] * np.sqrt(np.pi / self.p)
+
+    def overlap(self):
+        la, lb = self.sa.l, self.sb.l
+        S = [self._s1d(d) for d in range(3)]
+        out = np.empty((len(cart_comps(la)), len(cart_comps(lb))))
+        for i, (ax, ay, az) in enumerate(cart_comps(la)):
+            for j, (bx, by, bz) in enumerate(cart_comps(lb)):
+                out[i, j] = np.sum(self.cc * S[0][ax, bx] * S[1][ay, by] * S[2][az, bz])
+        return out
+
+    def kinetic(self):
+        """Needs kin=True (E tables extended to lb+2)."""
+        la, lb = self.sa.l, self.sb.l
+        b = np.broadcast_to(self.sb.exps[None, :], (self.sa.exps.size, self.sb.exps.size)).ravel()
+        S = [self._s1d(d) for d in range(3)]
+
+        def t1d(Sd, i, j):
+            v = -2.0 * b * b * Sd[i, j + 2] + b * (2 * j + 1) * Sd[i, j]
+            if j >= 2:
+                v = v - 0.5 * j * (j - 1) * Sd[i, j - 2]
+            return v
+        out = np.empty((len(cart_comps(la)), len(cart_comps(lb))))
+        for i, (ax, ay, az) in enumerate(cart_comps(la)):
+            for j, (bx, by, bz) in enumerate(cart_comps(lb)):
+                tx = t1d(S[0], ax, bx) * S[1][ay, by] * S[2][az, bz]
+                ty = S[0][ax, bx] * t1d(S[1], ay, by) * S[2][az, bz]
+                tz = S[0][ax, bx] * S[1][ay, by] * t1d(S[2], az, bz)
+                out[i, j] = np.sum(self.cc * (tx + ty + tz))
+        return out
+
+    def multipole1(self, origin):
+        """<a| (r - origin)_d |b> for d = x, y, z: (3, nca, ncb)."""
+        la, lb = self.sa.l, self.sb.l
+        S = [self._s1d(d) for d in range(3)]
+        M = []
+        for d in range(3):
+            e = self.E[d].reshape(self.E[d].shape[:3] + (-1,))
+            xpc = self.P[:, d] - origin[d]
+            M.append(((e[:, :, 1] if e.shape[2] > 1 else 0.0) + xpc * e[:, :, 0]) * np.sqrt(np.pi / self.p))
+        out = np.empty((3, len(cart_comps(la)), len(cart_comps(lb))))
+        for i, (ax, ay, az) in enumerate(cart_comps(la)):
+            for j, (bx, by, bz) in enumerate(cart_comps(lb)):
+                out[0, i, j] = np.sum(self.cc * M[0][ax, bx] * S[1][ay, by] * S[2][az, bz])
+                out[1, i, j] = np.sum(self.cc * S[0][ax, bx] * M[1][ay, by] * S[2][az, bz])
+                out[2, i, j] = np.sum(self.cc * S[0][ax, bx] * S[1][ay, by] * M[2][az, bz])
+        return out
+
+    def nuclear(self, charges, coords):
+        """sum_C -Z_C <a| 1/|r - C| |b> (point nuclei)."""
+        acc = np.zeros(self.Eab.shape[:2])
+        for z, c in zip(charges, coords):
+            d = self.P - c
+            R = hermite_r(self.L, self.p, d[:, 0], d[:, 1], d[:, 2])      # (ntuv, q)
+            acc += -z * np.einsum('abtq,tq->ab', self.Eab, R * (2.0 * np.pi / self.p))
+        return acc
+
+
+def eri_quartet(bra: ShellPair, ket: ShellPair) -> np.ndarray:
+    """(ab|cd) over Cartesian components: (nca, ncb, ncc, ncd)."""
+    p = bra.p[:, None]
+    q = ket.p[None, :]
+    alpha = p * q / (p + q)
+    d = bra.P[:, None, :] - ket.P[None, :, :]
+    L = bra.L + ket.L
+    R = hermite_r(L, alpha, d[..., 0], d[..., 1], d[..., 2])          # (ntuv_L, P, Q)
+    pref = 2.0 * np.pi ** 2.5 / (p * q * np.sqrt(p + q))
+    idx, sign = _sum_table(bra.L, ket.L)
+    Rm = R[idx] * pref                                                 # (ntab, ntcd, P, Q)
+    X = np.einsum('tsPQ,s,cdsQ->tcdP', Rm, sign, ket.Eab, optimize=True)
+    return np.einsum('abtP,tcdP->abcd', bra.Eab, X, optimize=True)
