@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--no-converge", action="store_true")
     ap.add_argument("--converge", action="store_true", help="also at N > 1")
     ap.add_argument("--nroots", type=int, default=20)
+    ap.add_argument("--k-mode", default="auto", choices=["auto", "direct", "stored"],
+                    help="exchange evaluation (xt_set_exchange_mode)")
     return ap.parse_args()
 
 
@@ -160,7 +162,8 @@ def main():
     t_setup = time.perf_counter()
     mf = make_device_mf(nao=args.nao, nc=args.nc, no=args.no, naux=naux, ngrid=ngrid,
                         xctype=args.xc, hyb=args.hyb, device=local, shard=(rank, world))
-    op = DeviceOperator(mf, "XTDA", shard=(rank, world), device=local, presharded=True)
+    op = DeviceOperator(mf, "XTDA", shard=(rank, world), device=local, presharded=True,
+                        k_mode=args.k_mode)
     mf.cderi = None
     mf.grids = None
     mf.fxc = None
@@ -210,10 +213,21 @@ def main():
     flops_launch = dom["flops"] / max(1, dom["launches"])
     achieved = flops_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     traffic = load_traffic(dom_name)
-    roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=FP64_PEAK_TFLOPS, unit="TFLOP/s",
-                    frac=round(achieved / FP64_PEAK_TFLOPS, 4), traffic=traffic,
-                    kernel=dom_name, avg_launch_ms=round(avg_ms, 4),
-                    flops_per_launch=flops_launch, launches_per_step=dom["launches"] / args.steps)
+    if dom_name == "mo_exchange_stored":
+        # HBM-bound: streams the stored exchange matrix once per launch (+ Ze in, sigma in/out)
+        ov = (args.nc + args.no) * (args.no + nv)
+        nzg = 2 * args.nvec
+        bytes_launch = 8.0 * (ov * ov + 3.0 * nzg * ov)
+        gbs = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        roofline = dict(bound="hbm", achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(gbs / HBM_PEAK_GBS, 4), traffic=traffic, kernel=dom_name,
+                        avg_launch_ms=round(avg_ms, 4), bytes_per_launch=bytes_launch,
+                        launches_per_step=dom["launches"] / args.steps)
+    else:
+        roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=FP64_PEAK_TFLOPS, unit="TFLOP/s",
+                        frac=round(achieved / FP64_PEAK_TFLOPS, 4), traffic=traffic,
+                        kernel=dom_name, avg_launch_ms=round(avg_ms, 4),
+                        flops_per_launch=flops_launch, launches_per_step=dom["launches"] / args.steps)
     others = {k: dict(ms_per_step=round(v["ms"] / args.steps, 3),
                       tflops=round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 3))
               for k, v in stats_acc.items()}
@@ -235,6 +249,7 @@ def main():
         gemm_classes=others,
         phases_ms_last_step=phases,
         setup_s=round(t_setup, 2),
+        exchange=dict(mode=op.k_mode, stored_gib=round(op.k_gib, 2), build_s=round(op.prepare_s, 3)),
     )
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -266,7 +281,9 @@ def main():
                                      lindep=1e-12, nroots=args.nroots, pick=pickeig, max_cycle=100,
                                      device=local, return_device=True)
         torch.cuda.synchronize()
-        result["converge"] = dict(nroots=args.nroots, wall_s=round(time.perf_counter() - tc, 2),
+        wall = time.perf_counter() - tc
+        result["converge"] = dict(nroots=args.nroots, wall_s=round(wall, 2),
+                                  wall_s_incl_exchange_build=round(wall + op.prepare_s, 2),
                                   iterations=int(icyc) + 1, converged=bool(np.all(conv)),
                                   e_min_ha=float(e[0]), criteria="|de|<1e-12, |r|<1e-5 (XTDA.py:775)")
     if rank == 0:

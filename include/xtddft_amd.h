@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define XT_ABI_VERSION 2
+#define XT_ABI_VERSION 3
 
 #define XT_PTR_HOST 0
 #define XT_PTR_DEVICE 1
@@ -105,6 +105,24 @@ int xt_set_grid(xt_ctx* ctx, const double* ao, const double* weights,
                 const double* kernel, int ptr_kind);
 /* XSF only: OO compression basis vects (no^2 x (no^2-1)) (XSF_TDA.py:397-414). */
 int xt_set_oo_basis(xt_ctx* ctx, const double* vects, int ptr_kind);
+
+/* exchange evaluation: the K part of get_jk / get_k (XTDA.py:518-543,
+   SF_TDA.py:273-281, XSF_TDA.py:996).  XT_K_DIRECT contracts the MO DF factor
+   per A.x (cost 2 naux nz O V^2); XT_K_STORED builds once per solve the MO
+   exchange matrix Kx[(i,a),(j,b)] = sum_P B_P[i,j] B_P[a,b] (x the hybrid
+   coefficients) and keeps it in HBM ((O V)^2 doubles per MO basis), making the
+   per-A.x exchange one HBM-streaming GEMM -- PySCF's incore-vs-direct choice
+   (mf._eri kept when it fits max_memory).  XT_K_AUTO (default) stores when
+   the matrix fits max_gib (<= 0: free HBM minus a reserve).  The XSF Delta-A
+   exchange blocks always run direct. */
+#define XT_K_AUTO 0
+#define XT_K_DIRECT 1
+#define XT_K_STORED 2
+int xt_set_exchange_mode(xt_ctx* ctx, int mode, double max_gib);
+/* Build what is built once per solve (the stored exchange matrix when the
+   mode resolves to it; xt_apply would otherwise build it on first use) and
+   report the resolved mode and its HBM footprint (GiB). */
+int xt_prepare(xt_ctx* ctx, int* k_mode, double* k_gib);
 
 /* the hot path --------------------------------------------------------- */
 /* sigma = A z for nz trial vectors, row-major (nz x dim) in the reference's

@@ -18,12 +18,35 @@ def rel(a, b):
     return np.abs(a - b).max() / np.abs(b).max()
 
 
-@pytest.fixture(scope="module")
-def dev(hiplib):
+@pytest.fixture(scope="module", params=["direct", "stored"])
+def dev(hiplib, request):
+    """DeviceOperator with the exchange forced to the DF sandwich or the stored MO matrix."""
+    import functools
     import torch
     assert torch.cuda.is_available(), "GPU tests need an MI355X"
     from xtddft_amd.operator import DeviceOperator
-    return DeviceOperator
+
+    def make(*a, **kw):
+        op = DeviceOperator(*a, k_mode=request.param, **kw)
+        assert op.k_mode == (request.param if _has_k(op.mf) else "direct")
+        return op
+    return make
+
+
+def _has_k(mf):
+    return mf.xctype == "HF" or mf.hyb != 0 or mf.omega != 0
+
+
+def test_exchange_mode_auto_respects_cap(hiplib):
+    from xtddft_amd.operator import DeviceOperator
+    mf = make_mf(nao=26, nc=5, no=2, xctype="GGA", hyb=0.2)
+    vind, hdiag = oxtda.gen_tda_operation(mf)
+    z = make_trial_vectors(3, hdiag.size)
+    big = DeviceOperator(mf, "XTDA")
+    small = DeviceOperator(mf, "XTDA", k_max_gib=1e-6)
+    assert big.k_mode == "stored" and big.k_gib > 0
+    assert small.k_mode == "direct" and small.k_gib == 0
+    assert rel(big.apply(z), vind(z)) < RTOL and rel(small.apply(z), vind(z)) < RTOL
 
 
 @pytest.mark.parametrize("case", list_cases())

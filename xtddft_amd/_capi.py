@@ -17,6 +17,8 @@ XT_PTR_HOST = 0
 XT_PTR_DEVICE = 1
 KIND = {"XTDA": 0, "UTDA": 1, "SF_DOWN": 2, "SF_UP": 3, "XSF": 4}
 XC = {"HF": 0, "LDA": 1, "GGA": 2}
+K_MODE = {"auto": 0, "direct": 1, "stored": 2}
+K_MODE_NAME = {v: k for k, v in K_MODE.items()}
 
 ERRORS = {-1: ValueError, -2: MemoryError, -3: RuntimeError, -4: RuntimeError, -5: RuntimeError}
 
@@ -25,7 +27,7 @@ EXPORTS = [
     "xt_set_orbitals", "xt_set_fock_mo", "xt_set_orbital_energies", "xt_set_jk_df",
     "xt_set_jk_eri8", "xt_naux",
     "xt_set_grid", "xt_set_oo_basis", "xt_apply", "xt_dim", "xt_last_timings",
-    "xt_xsf_j_diagonals", "xt_set_profile", "xt_profile_stats", "xt_dgemm", "xt_precond", "xt_row_norms2", "xt_row_scale",
+    "xt_xsf_j_diagonals", "xt_set_exchange_mode", "xt_prepare", "xt_set_profile", "xt_profile_stats", "xt_dgemm", "xt_precond", "xt_row_norms2", "xt_row_scale",
 ]
 
 
@@ -39,7 +41,7 @@ class XtDesc(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 2   # include/xtddft_amd.h XT_ABI_VERSION
+ABI_VERSION = 3   # include/xtddft_amd.h XT_ABI_VERSION
 
 
 class LibraryMissing(RuntimeError):
@@ -85,6 +87,8 @@ def lib():
     L.xt_dim.argtypes = [vp]
     L.xt_last_timings.argtypes = [vp, dp]
     L.xt_xsf_j_diagonals.argtypes = [vp, dp, dp, c_int]
+    L.xt_set_exchange_mode.argtypes = [vp, c_int, c_double]
+    L.xt_prepare.argtypes = [vp, POINTER(c_int), POINTER(c_double)]
     L.xt_set_profile.argtypes = [vp, c_int]
     L.xt_profile_stats.argtypes = [vp, c_int, dp]
     L.xt_dgemm.argtypes = [c_int, c_int, c_int, c_int, c_int, c_double, dp, c_long, dp, c_long,

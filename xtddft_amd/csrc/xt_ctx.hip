@@ -82,6 +82,12 @@ struct xt_ctx {
   double prof_ms[6] = {0, 0, 0, 0, 0, 0};
   int prof_launches[6] = {0, 0, 0, 0, 0, 0};
   int chol_rank = 0;         // full Cholesky rank of the last xt_set_jk_eri8
+  // exchange evaluation (xt_set_exchange_mode): stored MO exchange matrix per channel group
+  int kmode = XT_K_AUTO;
+  double k_max_bytes = 0.0;  // auto-mode cap (0: free HBM minus a reserve)
+  int k_resolved = -1;       // -1 undecided, 0 direct (DF sandwich), 1 stored
+  bool kx_valid = false;
+  DevBuf Kx;
 };
 
 static int dim_of(const xt_desc& d) {
@@ -206,7 +212,8 @@ int xt_destroy(xt_ctx* c) {
   (void)hipSetDevice(c->d.device);
   DevBuf* bufs[] = {&c->C, &c->Bmo, &c->Bmo_lr, &c->Phi, &c->kern, &c->F, &c->eps, &c->vects,
                     &c->ze, &c->acc, &c->kx, &c->zr, &c->tbuf, &c->ubuf, &c->gam, &c->gam2, &c->ws,
-                    &c->stage, &c->stage2, &c->zin, &c->sout, &c->trace, &c->zp, &c->accT, &c->wbuf};
+                    &c->stage, &c->stage2, &c->zin, &c->sout, &c->trace, &c->zp, &c->accT, &c->wbuf,
+                    &c->Kx};
   for (DevBuf* b : bufs) b->release();
   for (int i = 0; i < 5; ++i) (void)hipEventDestroy(c->ev[i]);
   for (hipEvent_t e : c->pev) (void)hipEventDestroy(e);
@@ -240,6 +247,7 @@ int xt_set_orbitals(xt_ctx* c, const double* ca, const double* cb, int ptr_kind)
     HIPCHK(hipMemcpyAsync(c->C.p + nn, cb, nn * 8, k, c->st));
   }
   c->has_orb = true;
+  c->kx_valid = false;
   return 0;
 }
 
@@ -336,6 +344,7 @@ int xt_set_jk_df(xt_ctx* c, const double* cderi, int which, int ptr_kind) {
   HIPCHK(hipStreamSynchronize(c->st));
   c->stage.release(); c->stage2.release();
   if (which == 0) c->has_df = true; else c->has_lr = true;
+  c->kx_valid = false; c->k_resolved = -1;
   return 0;
 }
 
@@ -420,6 +429,7 @@ int xt_set_jk_eri8(xt_ctx* c, const double* eri, int which, double tol, int p_ra
   c->d.naux = rows;
   c->chol_rank = rank;
   if (which == 0) c->has_df = true; else c->has_lr = true;
+  c->kx_valid = false; c->k_resolved = -1;
   return 0;
 }
 
@@ -666,6 +676,121 @@ static int exchange_main(xt_ctx* c, int nz, const DevBuf& B, double coef) {
       RET(gemm(c, g2));
     }
   }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Stored MO exchange (XT_K_STORED).  Per channel group g (occupied basis ob,
+// virtual basis vb) the exchange kernel of the sandwich above, contracted over
+// P once per solve and kept in HBM:
+//   Kx_g[(i,a),(j,b)] = ck sum_P Bo[P][i][j] Bv[P][v0+a][v0+b] + ck_lr (same, long range)
+// (symmetric under (i,a) <-> (j,b); (O V)^2 doubles per group).  Per A.x the
+// exchange is then one skinny GEMM  acc_g[x][(j,b)] -= sum_(i,a) Ze_g[x][(i,a)] Kx_g[(i,a),(j,b)],
+// streaming Kx once (HBM-bound, 2 nzg flops per 8 bytes) instead of the
+// 2 naux nzg O V^2 flops of the DF sandwich.  The reference makes the same
+// trade when PySCF keeps the ERIs incore (mf._eri, max_memory) rather than
+// running integral-direct J/K.
+// ---------------------------------------------------------------------------
+static size_t kx_doubles(const xt_ctx* c) {
+  Group gr[2];
+  const int ngr = channel_groups(c, gr);
+  const size_t ov = (size_t)c->O * c->V;
+  return ov * ov * (size_t)ngr;
+}
+
+static bool has_exchange(const xt_ctx* c) {
+  return (c->ck != 0.0 || c->ck_lr != 0.0) && c->d.naux > 0;
+}
+
+static int resolve_kmode(xt_ctx* c) {
+  if (c->k_resolved >= 0) return 0;
+  if (!has_exchange(c) || c->kmode == XT_K_DIRECT) { c->k_resolved = 0; return 0; }
+  if (c->kmode == XT_K_STORED) { c->k_resolved = 1; return 0; }
+  const size_t need = kx_doubles(c) * 8;
+  size_t cap;
+  if (c->k_max_bytes > 0) {
+    cap = (size_t)c->k_max_bytes;
+  } else {
+    size_t fr = 0, tot = 0;
+    HIPCHK(hipMemGetInfo(&fr, &tot));
+    fr += c->Kx.n * 8;                       // an existing matrix would be reused
+    size_t reserve = tot / 10;
+    if (reserve < ((size_t)24 << 30)) reserve = (size_t)24 << 30;   // XC chunks, Davidson subspace
+    cap = fr > reserve ? fr - reserve : 0;
+  }
+  c->k_resolved = need <= cap ? 1 : 0;
+  return 0;
+}
+
+static int build_kx(xt_ctx* c) {
+  const int O = c->O, V = c->V, nmo = c->d.nmo, naux = c->d.naux;
+  const long mm = (long)nmo * nmo;
+  const size_t ov = (size_t)O * V;
+  Group gr[2];
+  const int ngr = channel_groups(c, gr);
+  RET(c->Kx.ensure(ov * ov * ngr));
+  HIPCHK(hipMemsetAsync(c->Kx.p, 0, ov * ov * ngr * 8, c->st));
+  for (int q = 0; q < ngr; ++q) {
+    double* K = c->Kx.p + (size_t)q * ov * ov;
+    for (int pass = 0; pass < 2; ++pass) {
+      const double coef = pass ? c->ck_lr : c->ck;
+      if (coef == 0.0) continue;
+      const DevBuf& B = pass ? c->Bmo_lr : c->Bmo;
+      const double* Bo = bmo_of(c, B, gr[q].ob);
+      const double* Bv = bmo_of(c, B, gr[q].vb) + (long)c->v0 * nmo + c->v0;
+      for (int i = 0; i < O; ++i) {
+        // batch a: Kx[(i,a)][(j,b)] += coef sum_P Bo[P][i][j] Bv[P][a][b]
+        GemmDesc g;
+        g.M = O; g.N = V; g.K = naux; g.nb1 = V;
+        g.A = Bo + (long)i * nmo; g.sAm = 1; g.sAk = mm; g.sAb1 = 0;
+        g.B = Bv; g.sBk = mm; g.sBn = 1; g.sBb1 = nmo;
+        g.C = K + (size_t)i * V * ov; g.ldc = V; g.sCb1 = (long)ov;
+        g.alpha = coef; g.beta = 1.0;
+        RET(gemm(c, g));
+      }
+    }
+  }
+  HIPCHK(hipStreamSynchronize(c->st));
+  c->kx_valid = true;
+  return 0;
+}
+
+static int exchange_stored(xt_ctx* c, int nz) {
+  const size_t ov = (size_t)c->O * c->V;
+  const long chs = (long)nz * ov;
+  Group gr[2];
+  const int ngr = channel_groups(c, gr);
+  for (int q = 0; q < ngr; ++q) {
+    GemmDesc g;   // acc_g[x][(j,b)] -= sum_(i,a) Ze_g[x][(i,a)] Kx_g[(i,a)][(j,b)]
+    g.M = gr[q].nch * nz; g.N = (int)ov; g.K = (int)ov;
+    g.A = c->ze.p + gr[q].ch0 * chs; g.sAm = (long)ov; g.sAk = 1;
+    g.B = c->Kx.p + (size_t)q * ov * ov; g.sBk = (long)ov; g.sBn = 1;
+    g.C = c->acc.p + gr[q].ch0 * chs; g.ldc = (long)ov;
+    g.alpha = -1.0; g.beta = 1.0;
+    g.tag = 1;
+    RET(gemm(c, g));
+  }
+  return 0;
+}
+
+extern "C" int xt_set_exchange_mode(xt_ctx* c, int mode, double max_gib) {
+  if (!c) return fail(XT_ERR_ARG, "null ctx");
+  if (mode < XT_K_AUTO || mode > XT_K_STORED) return fail(XT_ERR_ARG, "bad exchange mode");
+  c->kmode = mode;
+  c->k_max_bytes = max_gib > 0 ? max_gib * (double)((size_t)1 << 30) : 0.0;
+  c->k_resolved = -1;
+  if (mode == XT_K_DIRECT) { c->Kx.release(); c->kx_valid = false; }
+  return 0;
+}
+
+extern "C" int xt_prepare(xt_ctx* c, int* k_mode, double* k_gib) {
+  if (!c) return fail(XT_ERR_ARG, "null ctx");
+  (void)hipSetDevice(c->d.device);
+  if (has_exchange(c) && !c->has_df) return fail(XT_ERR_STATE, "DF factor not set");
+  RET(resolve_kmode(c));
+  if (c->k_resolved == 1 && !c->kx_valid) RET(build_kx(c));
+  if (k_mode) *k_mode = c->k_resolved == 1 ? XT_K_STORED : XT_K_DIRECT;
+  if (k_gib) *k_gib = c->k_resolved == 1 ? kx_doubles(c) * 8.0 / (double)((size_t)1 << 30) : 0.0;
   return 0;
 }
 
@@ -960,8 +1085,14 @@ extern "C" int xt_apply(xt_ctx* c, int nz, const double* z, double* sigma, int p
                             c->acc.p + ch * chs, V, (long)O * V, 1.0));
     }
     if (has_k) {
-      RET(exchange_main(c, nz, c->Bmo, -c->ck));
-      if (c->ck_lr != 0.0) RET(exchange_main(c, nz, c->Bmo_lr, -c->ck_lr));
+      RET(resolve_kmode(c));
+      if (c->k_resolved == 1) {
+        if (!c->kx_valid) RET(build_kx(c));
+        RET(exchange_stored(c, nz));
+      } else {
+        RET(exchange_main(c, nz, c->Bmo, -c->ck));
+        if (c->ck_lr != 0.0) RET(exchange_main(c, nz, c->Bmo_lr, -c->ck_lr));
+      }
     }
     if (xsf && d.sa > 0) RET(xsf_delta_a(c, nz));
   }

@@ -69,8 +69,11 @@ def shape_info(mf: MeanField, kind: str):
 class DeviceOperator:
     def __init__(self, mf: MeanField, kind: str, *, sa: int = 0, foo: float = 1.0,
                  fglobal: float = 0.0, remove: bool = False, shard=(0, 1), device: int = 0,
-                 stream=None, presharded: bool = False):
-        """presharded: mf.cderi / mf.grids already hold only this rank's slice."""
+                 stream=None, presharded: bool = False, k_mode: str = "auto",
+                 k_max_gib: float = 0.0):
+        """presharded: mf.cderi / mf.grids already hold only this rank's slice.
+        k_mode: exchange evaluation ('auto' | 'direct' | 'stored', see
+        xt_set_exchange_mode); k_max_gib caps the stored matrix in auto mode."""
         L = _capi.lib()
         self.mf, self.kind = mf, kind
         rank, nranks = shard
@@ -110,6 +113,20 @@ class DeviceOperator:
         _capi.check(L.xt_set_stream(h, ctypes.c_void_p(stream or 0)), "xt_set_stream")
         self.dim = L.xt_dim(h)
         self._setup()
+        _capi.check(L.xt_set_exchange_mode(h, _capi.K_MODE[k_mode], float(k_max_gib)),
+                    "xt_set_exchange_mode")
+        self.prepare()
+
+    def prepare(self):
+        """Build the once-per-solve device data (stored exchange matrix when chosen)."""
+        import time
+        m, g = ctypes.c_int(), ctypes.c_double()
+        t0 = time.perf_counter()
+        _capi.check(self._L.xt_prepare(self._h, ctypes.byref(m), ctypes.byref(g)), "xt_prepare")
+        self.prepare_s = time.perf_counter() - t0     # xt_prepare synchronises the stream
+        self.k_mode = _capi.K_MODE_NAME[m.value]
+        self.k_gib = g.value
+        return self.k_mode
 
     # -------------------------------------------------------------- setup
     def _setup(self):
@@ -211,7 +228,10 @@ class DeviceOperator:
 
     def profile_stats(self):
         out = {}
-        for tag, name in self.PROFILE_TAGS.items():
+        names = dict(self.PROFILE_TAGS)
+        if getattr(self, "k_mode", "direct") == "stored":
+            names[1] = "mo_exchange_stored"
+        for tag, name in names.items():
             buf = (ctypes.c_double * 3)()
             _capi.check(self._L.xt_profile_stats(self._h, tag, ctypes.cast(buf, ctypes.c_void_p)), "stats")
             out[name] = dict(tag=tag, ms=buf[0], launches=int(buf[1]), flops=buf[2])
