@@ -20,9 +20,10 @@ TAGS = {1: "df_exchange_contract", 2: "xc_forward_u", 3: "xc_back_l", 4: "xc_for
 
 
 def tag_of(name):
+    """GEMM class of a dgemm_kernel<BM, BN, WGM, WGN, BK, MINW, A_KC, B_KC, TAG, MODE> symbol."""
     if "dgemm_kernel<" not in name:
         return None
-    t = int(name.split("dgemm_kernel<")[1].split(">")[0].split(",")[-1])
+    t = int(name.split("dgemm_kernel<")[1].split(">")[0].split(",")[8])
     return TAGS.get(t)
 
 
@@ -45,6 +46,14 @@ def durations(path):
 
 
 def main(prof_dir, rnd="r01"):
+    # the bench line names tag 1 after the exchange mode it ran
+    try:
+        with open(os.path.join(prof_dir, "trace.log")) as f:
+            line = [l for l in f if l.startswith("{")][-1]
+        if "mo_exchange_stored" in json.loads(line).get("gemm_classes", {}):
+            TAGS[1] = "mo_exchange_stored"
+    except Exception:
+        pass
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
     shutil.copy(os.path.join(prof_dir, "trace", "run_kernel_stats.csv"),

@@ -4,7 +4,7 @@
 #   2) PMC FETCH_SIZE pass, 3) PMC WRITE_SIZE pass (separate passes, MI355X_MICROARCH.md HBM section)
 set -euo pipefail
 export TMPDIR=/tmp
-OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/prof_r01
+OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/${PROF_TAG:-prof_r01}
 mkdir -p "$OUT"
 ARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline --no-converge"}
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 bench.py $ARGS > "$OUT/trace.log" 2>&1
