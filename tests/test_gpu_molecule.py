@@ -43,6 +43,9 @@ def test_xsf_tda_kernel_matches_reference(torch, kind, key, jk_mode):
     err = np.abs(np.asarray(e_ev) - ref).max() / HA2EV_XSF
     assert err < TOL_HA, (e_ev, ref)
     assert v.shape[1] == 10
+    if kind == "UKS":   # Delta<S^2> from the device eigenvectors (XSF_TDA.analyse)
+        ds, _ = x.analyse()
+        assert np.abs(np.asarray(ds) - reference_outputs()["usf_uks_alda0_delta_s2"]).max() < 1e-4
 
 
 def test_xtda_on_roks_molecule_matches_oracle(torch):

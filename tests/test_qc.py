@@ -133,3 +133,16 @@ def test_oracle_xsf_roots_match_reference(kind, key):
     e = np.linalg.eigvalsh(a)[:10] * HA2EV_XSF
     ref = np.asarray(reference_outputs()[key])
     assert np.abs(e - ref).max() / HA2EV_XSF < 1e-6, e - ref
+
+
+def test_usf_delta_s2_matches_reference():
+    """XSF_TDA.analyse Delta<S^2> on the UKS reference (XSF_TDA.py:613-649, 781-786)
+    from the oracle's eigenvectors, against the notebook's printed list."""
+    from xtddft_amd.xsf_tda import delta_s2_u
+    mfd = hf_meanfield("UKS")
+    o = oxsf.XSFOracle(mfd)
+    vind, hdiag = o.gen_tda_operation_sf(fglobal=oxsf.default_fglobal(mfd))
+    _, v = np.linalg.eigh(vind(np.eye(hdiag.size)).T)
+    ds = [delta_s2_u(mfd, v[:, n], o.nc, o.no, o.nv) - o.no + 1 for n in range(10)]
+    ref = reference_outputs()["usf_uks_alda0_delta_s2"]
+    assert np.abs(np.asarray(ds) - ref).max() < 1e-5

@@ -156,6 +156,11 @@ class MeanField:
     def get_hcore(self):
         return self.h1e
 
+    def get_ovlp(self):
+        """AO overlap (the SCF's when it supplied one; synthetic problems have S = I)."""
+        s = self.extra.get("s1e")
+        return np.eye(self.nao) if s is None else s
+
     def get_veff(self, mol=None, dm=None):
         return self.veff
 

@@ -43,6 +43,35 @@ def get_vect(no):
     return vects
 
 
+def split_xsf_vector(value, nc, no, nv, vects=None):
+    """cv (nc,nv), co (nc,no), ov (no,nv), oo (no,no) blocks of one XSF vector in
+    the reference's order; a compressed OO block is expanded with ``vects``
+    (XSF_TDA.py:728-734)."""
+    d1, d2, d3 = nc * nv, nc * nv + nc * no, nc * nv + nc * no + no * nv
+    oo = value[d3:]
+    oo = (vects @ oo).reshape(no, no) if vects is not None else oo.reshape(no, no)
+    return (value[:d1].reshape(nc, nv), value[d1:d2].reshape(nc, no),
+            value[d2:d3].reshape(no, nv), oo)
+
+
+def delta_s2_u(mf, value, nc, no, nv):
+    """XSF_TDA.deltaS2_U (XSF_TDA.py:613-649): the <S^2> term P_ab of a spin-flip
+    vector on a UKS reference, from the alpha/beta MO overlaps."""
+    mo, occ = mf.mo_coeff, mf.mo_occ
+    s = mf.get_ovlp()
+    mooa = mo[0][:, occ[0] > 0]
+    moob = mo[1][:, occ[1] > 0]
+    movb = mo[1][:, occ[1] == 0]
+    sba_oo = moob.T @ s @ mooa
+    sba_vo = movb.T @ s @ mooa
+    cv, co, ov, oo = split_xsf_vector(value, nc, no, nv)
+    x_ba = np.vstack([np.hstack([co, cv]), np.hstack([oo, ov])]).T    # (no+nv, nc+no)
+    t1 = np.einsum('ai,aj,jk,ki->', x_ba, x_ba, sba_oo.T, sba_oo)
+    t2 = np.einsum('ai,bi,kb,ak->', x_ba, x_ba, sba_vo.T, sba_vo)
+    t3 = np.einsum('ai,ai->', x_ba, sba_vo) ** 2
+    return t1 - t2 + t3
+
+
 class XSF_TDA:
     def __init__(self, mf: MeanField, SA=None, davidson=True, method=0, collinear_samples=60,
                  calculate_sp=False, device=0, shard=(0, 1)):
@@ -147,6 +176,41 @@ class XSF_TDA:
             vind, x0, hdiag, tol=1e-8, lindep=1e-9, nroots=self.nstates, max_cycle=1000,
             device=self.device)
         self.v = np.array(x1).T
+
+    def deltaS2_U(self, nstate):
+        """P_ab of root ``nstate`` (XSF_TDA.py:613-649), UKS references."""
+        return delta_s2_u(self.mf, np.asarray(self.v)[:, nstate], self.nc, self.no, self.nv)
+
+    def analyse(self, threshold=0.05, verbose=False):
+        """Delta<S^2> per root and the dominant-amplitude lines (XSF_TDA.py:709-793):
+        UKS: P_ab - no + 1; ROKS with SA = 0: -2 S + 1 + sum cv^2 - sum oo^2 +
+        (tr oo)^2; spin-adapted ROKS roots are pure spin states (no value, None).
+        Returns (Ds, lines); irrep labels need the point-group tables of PySCF
+        and are not reproduced."""
+        nc, no, nv = self.nc, self.no, self.nv
+        vects = self.vects if self.re else None
+        Ds, lines = [], []
+        for n in range(self.nstates):
+            value = np.asarray(self.v)[:, n]
+            cv, co, ov, oo = split_xsf_vector(value, nc, no, nv, vects)
+            for tag, blk, (o0, v0) in (("CV", cv, (0, nc + no)), ("CO", co, (0, nc)),
+                                       ("OV", ov, (nc, nc + no)), ("OO", oo, (nc, nc))):
+                for o, v in zip(*np.where(abs(blk) > threshold)):
+                    lines.append(f"{100 * blk[o, v] ** 2:5.2f}% {tag}(ab) {o + 1 + o0}a -> "
+                                 f"{v + 1 + v0}b {blk[o, v]:10.5f}")
+            if self.type_u:
+                ds2 = self.deltaS2_U(n) - no + 1
+            elif self.SA == 0:
+                ds2 = -2 * self.ground_s + 1 + (cv * cv).sum() - (oo * oo).sum() + np.trace(oo) ** 2
+            else:
+                ds2 = None
+            Ds.append(ds2)
+            lines.append(f"Excited state {n + 1} {self.e[n] * HA2EV_XSF:10.5f} eV "
+                         f"{self.e[n] + self.mf.e_tot:11.8f} Hartree"
+                         + (f" D<S^2>={ds2:3.2f}" if ds2 is not None else ""))
+        if verbose:
+            print("\n".join(lines))
+        return Ds, lines
 
     def get_Amat(self, foo=1.0, fglobal=None):
         """Explicit (remove-compressed when self.re) A through the device operator."""
