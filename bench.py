@@ -145,9 +145,17 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("for --gpus N > 1 launch with torch.distributed.run (one process per GPU)")
+    # XT_BENCH_BACKEND=gloo rehearses the N-rank path with ranks sharing the visible
+    # GPU(s) (tests on a one-GPU box); the real runs use nccl = RCCL over xGMI
+    backend = os.environ.get("XT_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     from xtddft_amd import build
     if rank == 0:
         build.build()
@@ -160,10 +168,15 @@ def main():
     ngrid = args.ngrid or 1200 * args.nao
     nv = args.nao - args.nc - args.no
     t_setup = time.perf_counter()
+    # stored exchange over N ranks: the MO factor is replicated and each rank
+    # keeps 1/N of the exchange rows (xt_set_partition); direct: aux-sliced factor
+    replicate = world > 1 and args.k_mode != "direct"
     mf = make_device_mf(nao=args.nao, nc=args.nc, no=args.no, naux=naux, ngrid=ngrid,
-                        xctype=args.xc, hyb=args.hyb, device=local, shard=(rank, world))
-    op = DeviceOperator(mf, "XTDA", shard=(rank, world), device=local, presharded=True,
-                        k_mode=args.k_mode)
+                        xctype=args.xc, hyb=args.hyb, device=local, shard=(rank, world),
+                        full_aux=replicate)
+    op = DeviceOperator(mf, "XTDA", shard=(rank, world), device=local,
+                        presharded="grid" if replicate else True, k_mode=args.k_mode,
+                        replicate_df=replicate)
     mf.cderi = None
     mf.grids = None
     mf.fxc = None
@@ -244,7 +257,10 @@ def main():
                               f"nocc*nvir={(args.nc + args.no) * nv}+{args.nc * (args.no + nv)}, "
                               f"nvec={args.nvec}, naux={naux}, ngrid={ngrid}, xc={args.xc}, hyb={args.hyb}"),
                     nao=args.nao, dim=op.dim, nvec=args.nvec, naux=naux, ngrid=ngrid,
-                    parallelism=f"aux+grid sharded x{world}, RCCL all-reduce of sigma"),
+                    parallelism=(f"grid sharded x{world}; " +
+                                 ("replicated MO DF factor, aux window + stored-exchange rows"
+                                  if replicate else "aux sharded") +
+                                 " per rank; RCCL all-reduce of sigma")),
         roofline=roofline,
         gemm_classes=others,
         phases_ms_last_step=phases,

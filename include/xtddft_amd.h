@@ -124,6 +124,14 @@ int xt_set_exchange_mode(xt_ctx* ctx, int mode, double max_gib);
    report the resolved mode and its HBM footprint (GiB). */
 int xt_prepare(xt_ctx* ctx, int* k_mode, double* k_gib);
 
+/* Rank partition of a sharded operator (one process per GPU):
+   the context keeps the whole MO factor but contracts J, the direct exchange
+   and the XSF Delta-A only over aux rows [p0, p1), and stores / applies only
+   the exchange rows whose occupied index is in [i0, i1) (superset O index).
+   Over ranks with disjoint windows and row blocks the partial sigma sum to
+   the full operator.  Defaults: all rows.  Call after the factor is set. */
+int xt_set_partition(xt_ctx* ctx, int p0, int p1, int i0, int i1);
+
 /* the hot path --------------------------------------------------------- */
 /* sigma = A z for nz trial vectors, row-major (nz x dim) in the reference's
    vector order (PySCF order for XTDA/UTDA/SF; cv|co|ov|oo for XSF, OO

@@ -155,6 +155,37 @@ def test_sharded_contexts_sum_to_full_operator(dev):
     assert rel(parts[0].apply(z) + parts[1].apply(z), vind(z)) < RTOL
 
 
+@pytest.mark.parametrize("replicate", [False, True])
+@pytest.mark.parametrize("case", ["xtda_rsh", "utda", "sf_up_u", "sf_down", "xsf_sa3", "xtda_eri8"])
+def test_partitioned_contexts_sum_to_full_operator(dev, case, replicate):
+    """Every kind: sum over 3 rank contexts == full operator, with the factor
+    aux-sliced or replicated + partitioned (aux window, stored-exchange rows)."""
+    from xtddft_amd.synthetic import as_eri8
+    kw, o = {}, None
+    if case == "xtda_rsh":
+        mf, kind = make_mf(nao=30, nc=6, no=2, xctype="GGA", hyb=0.2, omega=0.3, alpha=0.6), "XTDA"
+    elif case == "utda":
+        mf, kind = make_mf(nao=30, nc=6, no=2, xctype="LDA", kind="U", hyb=0.25), "UTDA"
+    elif case == "sf_up_u":
+        mf, kind = make_mf(nao=30, nc=6, no=2, xctype="GGA", kind="U", hyb=0.5), "SF_UP"
+    elif case == "sf_down":
+        mf, kind = make_mf(nao=30, nc=6, no=2, xctype="GGA", hyb=0.5), "SF_DOWN"
+    elif case == "xtda_eri8":
+        mf, kind = as_eri8(make_mf(nao=24, nc=5, no=2, xctype="GGA", hyb=0.2)), "XTDA"
+    else:
+        mf, kind = make_mf(nao=30, nc=6, no=3, xctype="GGA", hyb=0.5), "XSF"
+        o = oxsf.XSFOracle(mf, SA=3)
+        kw = dict(sa=3, fglobal=oxsf.default_fglobal(mf), remove=True)
+    full = dev(mf, kind, **kw)
+    parts = [dev(mf, kind, shard=(r, 3), replicate_df=replicate, **kw) for r in range(3)]
+    if o is not None:
+        for op in [full] + parts:
+            op.set_oo_basis(o.vects)
+    z = make_trial_vectors(4, full.dim)
+    assert all(p.replicate_df == replicate for p in parts)
+    assert rel(sum(p.apply(z) for p in parts), full.apply(z)) < RTOL
+
+
 # ---- stored ERIs (jk_mode ERI8): device pivoted Cholesky + the DF engine ----
 ERI8_TOL = 1e-11   # Cholesky to 1e-13 x max diagonal: exact to round-off at these sizes
 

@@ -88,6 +88,10 @@ struct xt_ctx {
   int k_resolved = -1;       // -1 undecided, 0 direct (DF sandwich), 1 stored
   bool kx_valid = false;
   DevBuf Kx;
+  // rank partition (xt_set_partition): aux window for J / direct exchange / XSF
+  // Delta-A over the resident factor, and the occupied rows of the stored exchange
+  int win_p0 = 0, win_np = -1;   // -1: all aux rows
+  int kr0 = 0, kr1 = -1;         // -1: all O rows
 };
 
 static int dim_of(const xt_desc& d) {
@@ -345,6 +349,7 @@ int xt_set_jk_df(xt_ctx* c, const double* cderi, int which, int ptr_kind) {
   c->stage.release(); c->stage2.release();
   if (which == 0) c->has_df = true; else c->has_lr = true;
   c->kx_valid = false; c->k_resolved = -1;
+  c->win_p0 = 0; c->win_np = -1;
   return 0;
 }
 
@@ -430,6 +435,7 @@ int xt_set_jk_eri8(xt_ctx* c, const double* eri, int which, double tol, int p_ra
   c->chol_rank = rank;
   if (which == 0) c->has_df = true; else c->has_lr = true;
   c->kx_valid = false; c->k_resolved = -1;
+  c->win_p0 = 0; c->win_np = -1;
   return 0;
 }
 
@@ -498,9 +504,17 @@ int xt_set_oo_basis(xt_ctx* c, const double* vects, int ptr_kind) {
 // ---------------------------------------------------------------------------
 // building blocks
 // ---------------------------------------------------------------------------
-static inline const double* bmo_of(xt_ctx* c, const DevBuf& B, int basis) {
+// aux rows this context contracts over (its window of the resident factor)
+static inline int naux_w(const xt_ctx* c) { return c->win_np < 0 ? c->d.naux : c->win_np; }
+// basis block of an MO factor, full rows / from the window start
+static inline const double* bmo_full(const xt_ctx* c, const DevBuf& B, int basis) {
   return B.p + (size_t)basis * c->d.naux * c->d.nmo * c->d.nmo;
 }
+static inline const double* bmo_of(xt_ctx* c, const DevBuf& B, int basis) {
+  return bmo_full(c, B, basis) + (size_t)c->win_p0 * c->d.nmo * c->d.nmo;
+}
+static inline int krow0(const xt_ctx* c) { return c->kr0; }
+static inline int krow1(const xt_ctx* c) { return c->kr1 < 0 ? c->O : c->kr1; }
 
 // S[x] += coef * sum_P Bo[P, ry0:+nry, rx0:+nrx] Z[x] Bv[P, cx0:+ncx, cy0:+ncy]
 // Z[x] at Z + x*svZ with row stride ldZ; S[x] at S + x*svS, row stride ldS.
@@ -508,7 +522,8 @@ static int sandwich(xt_ctx* c, const double* Bo, const double* Bv, int nz,
                     int ry0, int nry, int rx0, int nrx, int cx0, int ncx, int cy0, int ncy,
                     const double* Z, long ldZ, long svZ, double* S, long ldS, long svS, double coef) {
   if (nry <= 0 || nrx <= 0 || ncx <= 0 || ncy <= 0 || coef == 0.0) return 0;
-  const int naux = c->d.naux, nmo = c->d.nmo;
+  const int naux = naux_w(c), nmo = c->d.nmo;
+  if (naux <= 0) return 0;
   const long mm = (long)nmo * nmo;
   const double left = 2.0 * nry * nrx * (double)nz * ncx + 2.0 * nry * (double)nz * ncx * ncy;
   const double right = 2.0 * (double)nz * nrx * ncx * ncy + 2.0 * nry * nrx * (double)nz * ncy;
@@ -573,10 +588,10 @@ static int coulomb_gamma(xt_ctx* c, const double* B, int nz, int r0, int nr, int
                          const double* Z, long ldZ, long svZ, double* gam, double beta) {
   const int nmo = c->d.nmo;
   GemmDesc g;
-  g.M = nz; g.N = c->d.naux; g.K = ncl; g.R = nr;
+  g.M = nz; g.N = naux_w(c); g.K = ncl; g.R = nr;
   g.A = Z; g.sAm = svZ; g.sAk = 1; g.sAr = ldZ;
   g.B = B + (long)r0 * nmo + c0; g.sBn = (long)nmo * nmo; g.sBk = 1; g.sBr = nmo;
-  g.C = gam; g.ldc = c->d.naux; g.beta = beta;
+  g.C = gam; g.ldc = naux_w(c); g.beta = beta;
   return gemm(c, g);
 }
 
@@ -585,8 +600,8 @@ static int coulomb_project(xt_ctx* c, const double* B, int nz, int r0, int nr, i
                            const double* gam, double* S, long ldS, long svS, double coef) {
   const int nmo = c->d.nmo;
   GemmDesc g;
-  g.M = nz; g.N = ncl; g.K = c->d.naux; g.nb1 = nr;
-  g.A = gam; g.sAm = c->d.naux; g.sAk = 1;
+  g.M = nz; g.N = ncl; g.K = naux_w(c); g.nb1 = nr;
+  g.A = gam; g.sAm = naux_w(c); g.sAk = 1;
   g.B = B + (long)r0 * nmo + c0; g.sBk = (long)nmo * nmo; g.sBn = 1; g.sBb1 = nmo;
   g.C = S; g.ldc = svS; g.sCb1 = ldS;
   g.alpha = coef; g.beta = 1.0;
@@ -643,8 +658,9 @@ static int channel_groups(const xt_ctx* c, Group* g) {
 // accT_g[(j,x)][b] += coef * sum_P sum_{i,a} B[P][j][i] Zp_g[i][x][a] B[P][v0+a][v0+b]
 static int exchange_main(xt_ctx* c, int nz, const DevBuf& B, double coef) {
   if (coef == 0.0) return 0;
-  const int O = c->O, V = c->V, nmo = c->d.nmo, naux = c->d.naux;
+  const int O = c->O, V = c->V, nmo = c->d.nmo, naux = naux_w(c);
   const long mm = (long)nmo * nmo, chs = (long)nz * O * V;
+  if (naux <= 0) return 0;
   Group gr[2];
   const int ngr = channel_groups(c, gr);
   for (int q = 0; q < ngr; ++q) {
@@ -695,11 +711,21 @@ static size_t kx_doubles(const xt_ctx* c) {
   Group gr[2];
   const int ngr = channel_groups(c, gr);
   const size_t ov = (size_t)c->O * c->V;
-  return ov * ov * (size_t)ngr;
+  return (size_t)(krow1(c) - krow0(c)) * c->V * ov * (size_t)ngr;
 }
 
 static bool has_exchange(const xt_ctx* c) {
   return (c->ck != 0.0 || c->ck_lr != 0.0) && c->d.naux > 0;
+}
+
+extern "C" int xt_set_partition(xt_ctx* c, int p0, int p1, int i0, int i1) {
+  if (!c) return fail(XT_ERR_ARG, "null ctx");
+  if (p0 < 0 || p1 < p0 || p1 > c->d.naux) return fail(XT_ERR_ARG, "aux window outside [0, naux]");
+  if (i0 < 0 || i1 < i0 || i1 > c->O) return fail(XT_ERR_ARG, "exchange rows outside [0, O]");
+  c->win_p0 = p0; c->win_np = p1 - p0;
+  c->kr0 = i0; c->kr1 = i1;
+  c->kx_valid = false; c->k_resolved = -1;
+  return 0;
 }
 
 static int resolve_kmode(xt_ctx* c) {
@@ -726,19 +752,22 @@ static int build_kx(xt_ctx* c) {
   const int O = c->O, V = c->V, nmo = c->d.nmo, naux = c->d.naux;
   const long mm = (long)nmo * nmo;
   const size_t ov = (size_t)O * V;
+  const int i0 = krow0(c), i1 = krow1(c);
+  const size_t blk = (size_t)(i1 - i0) * V * ov;   // this context's rows of one group
   Group gr[2];
   const int ngr = channel_groups(c, gr);
-  RET(c->Kx.ensure(ov * ov * ngr));
-  HIPCHK(hipMemsetAsync(c->Kx.p, 0, ov * ov * ngr * 8, c->st));
+  if (blk == 0) { c->kx_valid = true; return 0; }
+  RET(c->Kx.ensure(blk * ngr));
+  HIPCHK(hipMemsetAsync(c->Kx.p, 0, blk * ngr * 8, c->st));
   for (int q = 0; q < ngr; ++q) {
-    double* K = c->Kx.p + (size_t)q * ov * ov;
+    double* K = c->Kx.p + (size_t)q * blk - (size_t)i0 * V * ov;   // row (i,a) at (i V + a) ov
     for (int pass = 0; pass < 2; ++pass) {
       const double coef = pass ? c->ck_lr : c->ck;
       if (coef == 0.0) continue;
       const DevBuf& B = pass ? c->Bmo_lr : c->Bmo;
-      const double* Bo = bmo_of(c, B, gr[q].ob);
-      const double* Bv = bmo_of(c, B, gr[q].vb) + (long)c->v0 * nmo + c->v0;
-      for (int i = 0; i < O; ++i) {
+      const double* Bo = bmo_full(c, B, gr[q].ob);   // all aux rows: Kx sums over every P
+      const double* Bv = bmo_full(c, B, gr[q].vb) + (long)c->v0 * nmo + c->v0;
+      for (int i = i0; i < i1; ++i) {
         // batch a: Kx[(i,a)][(j,b)] += coef sum_P Bo[P][i][j] Bv[P][a][b]
         GemmDesc g;
         g.M = O; g.N = V; g.K = naux; g.nb1 = V;
@@ -758,13 +787,16 @@ static int build_kx(xt_ctx* c) {
 static int exchange_stored(xt_ctx* c, int nz) {
   const size_t ov = (size_t)c->O * c->V;
   const long chs = (long)nz * ov;
+  const int i0 = krow0(c), i1 = krow1(c);
+  const size_t blk = (size_t)(i1 - i0) * c->V * ov;
+  if (blk == 0) return 0;
   Group gr[2];
   const int ngr = channel_groups(c, gr);
   for (int q = 0; q < ngr; ++q) {
-    GemmDesc g;   // acc_g[x][(j,b)] -= sum_(i,a) Ze_g[x][(i,a)] Kx_g[(i,a)][(j,b)]
-    g.M = gr[q].nch * nz; g.N = (int)ov; g.K = (int)ov;
-    g.A = c->ze.p + gr[q].ch0 * chs; g.sAm = (long)ov; g.sAk = 1;
-    g.B = c->Kx.p + (size_t)q * ov * ov; g.sBk = (long)ov; g.sBn = 1;
+    GemmDesc g;   // acc_g[x][(j,b)] -= sum_{(i,a), i in [i0,i1)} Ze_g[x][(i,a)] Kx_g[(i,a)][(j,b)]
+    g.M = gr[q].nch * nz; g.N = (int)ov; g.K = (i1 - i0) * c->V;
+    g.A = c->ze.p + gr[q].ch0 * chs + (long)i0 * c->V; g.sAm = (long)ov; g.sAk = 1;
+    g.B = c->Kx.p + (size_t)q * blk; g.sBk = (long)ov; g.sBn = 1;
     g.C = c->acc.p + gr[q].ch0 * chs; g.ldc = (long)ov;
     g.alpha = -1.0; g.beta = 1.0;
     g.tag = 1;
@@ -931,8 +963,8 @@ static int xsf_delta_a(xt_ctx* c, int nz) {
   }
   const double* B = bmo_of(c, c->Bmo, 0);
   // J parts: gamma_co, gamma_ov
-  RET(c->gam.ensure((size_t)nz * d.naux));
-  RET(c->gam2.ensure((size_t)nz * d.naux));
+  RET(c->gam.ensure((size_t)nz * naux_w(c) + 1));
+  RET(c->gam2.ensure((size_t)nz * naux_w(c) + 1));
   RET(coulomb_gamma(c, B, nz, mc, nc, mo_, no, Zco, ld, sv, c->gam.p, 0.0));
   RET(coulomb_gamma(c, B, nz, mo_, no, mv, nv, Zov, ld, sv, c->gam2.p, 0.0));
   RET(coulomb_project(c, B, nz, mc, nc, mo_, no, c->gam.p, Sco, ld, sv, -fg / tsm1));
@@ -1075,8 +1107,8 @@ extern "C" int xt_apply(xt_ctx* c, int nz, const double* z, double* sigma, int p
   // ---- Coulomb / exchange ----------------------------------------------------
   const bool has_k = (c->ck != 0.0 || c->ck_lr != 0.0);
   if (d.naux > 0) {
-    if (!sf) {   // J (spin-conserving only)
-      RET(c->gam.ensure((size_t)nz * d.naux));
+    if (!sf && naux_w(c) > 0) {   // J (spin-conserving only)
+      RET(c->gam.ensure((size_t)nz * naux_w(c)));
       for (int ch = 0; ch < nch; ++ch)
         RET(coulomb_gamma(c, bmo_of(c, c->Bmo, c->occ_basis[ch]), nz, 0, O, c->v0, V,
                           c->ze.p + ch * chs, V, (long)O * V, c->gam.p, ch == 0 ? 0.0 : 1.0));
@@ -1094,7 +1126,7 @@ extern "C" int xt_apply(xt_ctx* c, int nz, const double* z, double* sigma, int p
         if (c->ck_lr != 0.0) RET(exchange_main(c, nz, c->Bmo_lr, -c->ck_lr));
       }
     }
-    if (xsf && d.sa > 0) RET(xsf_delta_a(c, nz));
+    if (xsf && d.sa > 0 && naux_w(c) > 0) RET(xsf_delta_a(c, nz));
   }
   HIPCHK(hipEventRecord(c->ev[2], c->st));
 

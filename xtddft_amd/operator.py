@@ -6,9 +6,13 @@ This is the object behind every ``vind`` the reference API hands out
 ``torch`` CUDA tensors (device); trial vectors keep their kind on return.
 
 Sharding (multi-GPU, one process per GPU): ``shard=(rank, nranks)`` keeps
-1/nranks of the DF aux index P and of the grid points on this rank and adds
-the one-electron terms on rank 0 only, so the per-rank sigma are partial sums
-that ``xtddft_amd.parallel.allreduce_sigma`` combines.
+1/nranks of the grid points on this rank and adds the one-electron terms on
+rank 0 only, so the per-rank sigma are partial sums that
+``xtddft_amd.parallel.allreduce_sigma`` combines.  The DF
+factor is either sliced by aux index (``replicate_df=False``: each rank holds
+1/nranks of P) or replicated with an aux *window* plus a row block of the
+stored exchange matrix (``xt_set_partition``; the default unless the exchange
+is forced direct), so the stored exchange is split over the ranks too.
 """
 from __future__ import annotations
 
@@ -69,11 +73,14 @@ def shape_info(mf: MeanField, kind: str):
 class DeviceOperator:
     def __init__(self, mf: MeanField, kind: str, *, sa: int = 0, foo: float = 1.0,
                  fglobal: float = 0.0, remove: bool = False, shard=(0, 1), device: int = 0,
-                 stream=None, presharded: bool = False, k_mode: str = "auto",
-                 k_max_gib: float = 0.0):
-        """presharded: mf.cderi / mf.grids already hold only this rank's slice.
+                 stream=None, presharded=False, k_mode: str = "auto",
+                 k_max_gib: float = 0.0, replicate_df=None):
+        """presharded: True -- mf.cderi / mf.grids hold only this rank's slices;
+        "grid" -- only mf.grids is this rank's slice (mf.cderi is whole).
         k_mode: exchange evaluation ('auto' | 'direct' | 'stored', see
-        xt_set_exchange_mode); k_max_gib caps the stored matrix in auto mode."""
+        xt_set_exchange_mode); k_max_gib caps the stored matrix in auto mode.
+        replicate_df: keep the whole factor on every rank and partition by aux
+        window + exchange rows (default: k_mode != 'direct')."""
         L = _capi.lib()
         self.mf, self.kind = mf, kind
         rank, nranks = shard
@@ -83,11 +90,15 @@ class DeviceOperator:
         naux = mf.naux
         ngrid = mf.grids.ngrid if (mf.grids is not None and mf.xctype != "HF") else 0
         self.shard = (rank, nranks)
-        if presharded:
+        if replicate_df is None:
+            replicate_df = k_mode != "direct" and presharded is not True
+        self.replicate_df = bool(replicate_df) and nranks > 1
+        if presharded is True:
             self.aux_range, self.grid_range = (0, naux), (0, ngrid)
         else:
-            self.aux_range = _split(naux, rank, nranks)
-            self.grid_range = _split(ngrid, rank, nranks)
+            self.aux_range = (0, naux) if (self.replicate_df or presharded == "grid") \
+                else _split(naux, rank, nranks)
+            self.grid_range = (0, ngrid) if presharded == "grid" else _split(ngrid, rank, nranks)
         d = _capi.XtDesc()
         d.kind = _capi.KIND[kind]
         d.restricted = 1 if mf.is_rohf else 0
@@ -113,9 +124,21 @@ class DeviceOperator:
         _capi.check(L.xt_set_stream(h, ctypes.c_void_p(stream or 0)), "xt_set_stream")
         self.dim = L.xt_dim(h)
         self._setup()
+        if self.replicate_df:
+            self._set_partition(kind, nc, no)
         _capi.check(L.xt_set_exchange_mode(h, _capi.K_MODE[k_mode], float(k_max_gib)),
                     "xt_set_exchange_mode")
         self.prepare()
+
+    def _set_partition(self, kind, nc, no):
+        """Aux window and exchange row block of this rank (xt_set_partition)."""
+        rank, nranks = self.shard
+        naux_local, _ = self.naux()
+        p0, p1 = _split(naux_local, rank, nranks)
+        occ = nc if kind == "SF_UP" else nc + no
+        i0, i1 = _split(occ, rank, nranks)
+        _capi.check(self._L.xt_set_partition(self._h, p0, p1, i0, i1), "xt_set_partition")
+        self.partition = dict(aux=(p0, p1), exchange_rows=(i0, i1))
 
     def prepare(self):
         """Build the once-per-solve device data (stored exchange matrix when chosen)."""
@@ -149,8 +172,9 @@ class DeviceOperator:
         p0, p1 = self.aux_range
         if mf.jk_mode == "ERI8":
             # stored ERIs: factorised on the device; this rank keeps its block
-            # of Cholesky vectors (aux sharding)
-            rank, nranks = self.shard
+            # of Cholesky vectors (aux sharding) or all of them
+            # (replicated factor, partitioned by window)
+            rank, nranks = self.shard if not self.replicate_df else (0, 1)
             for which, eri in ((0, mf.eri), (1, mf.eri_lr if mf.omega != 0 else None)):
                 if eri is None:
                     continue

@@ -176,7 +176,7 @@ def as_eri8(mf: MeanField, chol_tol: float = 0.0) -> MeanField:
 
 
 def make_device_mf(nao=1000, nc=99, no=2, naux=None, ngrid=None, xctype="GGA", hyb=0.2,
-                   seed=DEFAULT_SEED, device=0, shard=(0, 1)) -> MeanField:
+                   seed=DEFAULT_SEED, device=0, shard=(0, 1), full_aux=False) -> MeanField:
     """Synthetic ROKS problem whose big tensors are generated directly in HBM.
 
     Same distributions as ``make_mf`` (torch RNG, so not bitwise equal): the
@@ -184,7 +184,8 @@ def make_device_mf(nao=1000, nc=99, no=2, naux=None, ngrid=None, xctype="GGA", h
     (aux rows / grid points ``shard = (rank, nranks)``), scaled with the
     GLOBAL sizes so every shard count describes the same operator statistics.
     Small per-orbital data (C, Fock, energies) come from ``make_mf`` and are
-    identical on every rank.
+    identical on every rank.  full_aux: every rank generates the whole DF
+    factor (same values on all ranks; the replicated-factor partition).
     """
     import torch
     naux = naux if naux is not None else 3 * nao
@@ -200,8 +201,12 @@ def make_device_mf(nao=1000, nc=99, no=2, naux=None, ngrid=None, xctype="GGA", h
         base, rem = divmod(n, nranks)
         lo = rank * base + min(rank, rem)
         return lo, lo + base + (1 if rank < rem else 0)
-    p0, p1 = split(naux)
+    p0, p1 = (0, naux) if full_aux else split(naux)
     g0, g1 = split(ngrid)
+    gaux = g
+    if full_aux:       # rank-independent stream for the replicated factor
+        gaux = torch.Generator(device=dev)
+        gaux.manual_seed(seed + 104729)
     nocc, nvir = nc + no, no + nv
     k = torch.arange(nao, device=dev, dtype=torch.float64)
     dmat = torch.exp(-torch.abs(k[:, None] - k[None, :]) / 50.0)
@@ -209,7 +214,7 @@ def make_device_mf(nao=1000, nc=99, no=2, naux=None, ngrid=None, xctype="GGA", h
     cderi = torch.empty((p1 - p0, nao, nao), dtype=torch.float64, device=dev)
     for q0 in range(0, p1 - p0, 64):
         q1 = min(p1 - p0, q0 + 64)
-        t = torch.randn((q1 - q0, nao, nao), dtype=torch.float64, device=dev, generator=g)
+        t = torch.randn((q1 - q0, nao, nao), dtype=torch.float64, device=dev, generator=gaux)
         cderi[q0:q1] = (t + t.transpose(1, 2)) * s * dmat
         del t
     ncomp = 4 if xctype == "GGA" else 1
