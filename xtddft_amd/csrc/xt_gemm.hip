@@ -53,14 +53,36 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 #define XT_INLINE __attribute__((always_inline))
 constexpr int GROUP_M = 8;       // m-tiles per grouped sweep over n (L2 panel reuse)
 
+// Sum of v over the four 16-lane rows of the wave (lanes l, l^16, l^32, l^48),
+// identical in every lane, on the VALU: v_permlane16/32_swap of a register with
+// itself leaves row pairs split across the two results, whose sum is the pair
+// sum in every lane (ds_bpermute-based __shfl_xor goes through the LDS pipe).
+__device__ __forceinline__ double rows_sum4(double v) {
+  auto pair16 = [](double x) XT_INLINE {
+    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+  };
+  auto pair32 = [](double x) XT_INLINE {
+    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+  };
+  return pair32(pair16(v));
+}
+
 // TAG only gives hot call sites their own kernel symbol (rocprofv3 identity).
 // MINW = waves per SIMD the register budget must allow (occupancy target).
 // MODE: 0 plain GEMM, 1 / 2 fused XC contractions (XcFuse, xt_internal.h).
 template <int BM, int BN, int WGM, int WGN, int BK, int MINW, bool A_KC, bool B_KC, int TAG, int MODE = 0>
 __global__ void __launch_bounds__(64 * WGM * WGN, MINW)
 dgemm_kernel(GemmParams p) {
-  static_assert(MODE == 0 || (BM == 128 && BN == 128 && WGM == 2 && WGN == 4 && !A_KC && B_KC),
-                "fused XC modes run on the 128x128 8-wave tile, A MN-contiguous, B staged K-contiguous");
+  static_assert(MODE == 0 || (BM == 128 && WGM * WGN == 8 && !A_KC && B_KC),
+                "fused XC modes run on 128-row 8-wave tiles, A MN-contiguous, B staged K-contiguous");
+  static_assert(MODE != 2 || BN == 128, "mode 2 staging map assumes a 128x128 tile");
+  static_assert(MODE != 2 || (WGM == 2 && WGN == 4), "mode 2 staging map assumes 2x4 waves");
   constexpr int LDP = BK + 1;
   constexpr int NTHREADS = 64 * WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;    // wave tile
@@ -74,7 +96,9 @@ dgemm_kernel(GemmParams p) {
   constexpr int B_STEP = B_KC ? NTHREADS / BK : NTHREADS / BN;
   static_assert(NTHREADS % BK == 0 && NTHREADS % BM == 0 && NTHREADS % BN == 0, "staging map");
 
-  __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
+  // mode 1 also stages the gradient weights of the current a-block (3 BN rows of 16, pitch 17)
+  constexpr int WSZ = MODE == 1 ? 3 * BN * 17 : 0;
+  __shared__ __attribute__((aligned(16))) double smem[2 * STAGE + WSZ];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -281,9 +305,10 @@ dgemm_kernel(GemmParams p) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
+          for (int j = 0; j < TN; ++j) {
             if ((!k_edge || 4 * s < kv) && (!mn_edge || (i < mi && j < nj)))
               acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af1[i], bf1[j], acc[i][j], 0, 0, 0);
+          }
       }
       return;
     }
@@ -339,47 +364,67 @@ dgemm_kernel(GemmParams p) {
     compute(buf, MN_EDGE, std::true_type{}, p.K - kt * BK);
   };
   if constexpr (MODE == 1) {
-    // rho forward: one a-block (16 a of 8 xg) per r; after its last K-tile the
-    // accumulators (W for 128 grid points) are contracted with the gradient
-    // weights and reduced over a; lane q keeps xg_l = 4 wm + q.
-    static_assert(TM == 4, "lane-q ownership of the 4 row sub-tiles");
-    double racc[TN][3];
+    // rho forward: one a-block (16 a of the block's xg) per r; after its last
+    // K-tile the accumulators (W for the block's grid points) are contracted with
+    // the gradient weights and reduced over a.  Row sub-tile i holds
+    // xg_l = wm TM + i (16 a each); lane q keeps the sub-tiles i = q (mod 4).
+    // Runs at two blocks per CU (128-register budget): one block's reduction
+    // overlaps the other's MFMAs.
+    static_assert(TM % 4 == 0, "lane-q ownership of the row sub-tiles");
+    constexpr int TQ = TM / 4;
+    double racc[TQ][TN][3];
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int u = 0; u < TQ; ++u)
 #pragma unroll
-      for (int c = 0; c < 3; ++c) racc[j][c] = 0.0;
-    // gradient weights w_c[g][a] of this lane's column sub-tile j, a = 16 r + q + 4 t
-    auto load_w = [&](int r, int j, double (&w)[3][4]) XT_INLINE {
-      const int g = min(n0 + wn * WN + j * 16 + r16, p.N - 1);
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int a = 16 * r + q + 4 * t;
-        const int acl = a < p.fz.V ? a : p.fz.V - 1;
+        for (int c = 0; c < 3; ++c) racc[u][j][c] = 0.0;
+    // Gradient weights w_c[g][a] of the block's columns and a-block r, staged
+    // through LDS after the a-block's last K-tile: sw[(c BN + n) 17 + a_l] (odd
+    // pitch: the reads in reduce(), 16 lanes = 16 n at one a_l, hit 16 distinct
+    // bank pairs).  a >= V is stored as 0.
+    constexpr int WP = 17;
+    static_assert((3 * BN * 16) % NTHREADS == 0, "w staging map");
+    constexpr int W_ELEMS = 3 * BN * 16 / NTHREADS;
+    double wl[W_ELEMS];
+    auto load_w = [&](int r) XT_INLINE {
+      const int a = 16 * r + (tid & 15);
+      const int acl = a < p.fz.V ? a : p.fz.V - 1;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) w[c][t] = p.fz.w[c * p.fz.wc + (long)g * p.fz.wg + acl];
+      for (int e = 0; e < W_ELEMS; ++e) {
+        const int cn = (tid >> 4) + e * (NTHREADS / 16), c = cn / BN, n = cn % BN;
+        const int g = min(n0 + n, p.N - 1);
+        wl[e] = p.fz.w[c * p.fz.wc + (long)g * p.fz.wg + acl];
       }
     };
-    // contract sub-tile column j of the accumulators with its weights, reduce
-    // over the 16 a of each row sub-tile (4 in-lane + 4 lanes q), clear it
-    auto reduce_j = [&](int r, int j, const double (&w)[3][4]) XT_INLINE {
-      double wz[3][4];
+    auto store_w = [&](int r) XT_INLINE {
+      const bool ok = 16 * r + (tid & 15) < p.fz.V;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const bool ok = 16 * r + q + 4 * t < p.fz.V;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) wz[c][t] = ok ? w[c][t] : 0.0;
+      for (int e = 0; e < W_ELEMS; ++e) {
+        const int cn = (tid >> 4) + e * (NTHREADS / 16);
+        smem[2 * STAGE + cn * WP + (tid & 15)] = ok ? wl[e] : 0.0;
       }
+    };
+    // contract the accumulators with the weights, reduce over the 16 a of each
+    // row sub-tile (4 in-lane, 4 rows of lanes by rows_sum4), clear them
+    auto reduce = [&]() XT_INLINE {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
+      for (int j = 0; j < TN; ++j) {
+        const int n = wn * WN + j * 16 + r16;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-          double sv = acc[i][j][0] * wz[c][0] + acc[i][j][1] * wz[c][1] + acc[i][j][2] * wz[c][2] +
-                      acc[i][j][3] * wz[c][3];
-          sv += __shfl_xor(sv, 16);
-          sv += __shfl_xor(sv, 32);
-          if (q == i) racc[j][c] += sv;
+          double wz[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) wz[t] = smem[2 * STAGE + (c * BN + n) * WP + q + 4 * t];
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const double sv = rows_sum4(acc[i][j][0] * wz[0] + acc[i][j][1] * wz[1] +
+                                        acc[i][j][2] * wz[2] + acc[i][j][3] * wz[3]);
+            if ((i & 3) == q) racc[i >> 2][j][c] += sv;
+          }
         }
-        acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
       }
     };
     auto run1 = [&](auto MN_EDGE) XT_INLINE {
@@ -402,26 +447,30 @@ dgemm_kernel(GemmParams p) {
         store_tile(buf ^ 1, kv);
         __syncthreads();
         buf ^= 1;
-        // (prefetching w behind the last K-tile costs 30 VGPRs and measured slower)
-        double w[3][4];
-        load_w(r, 0, w);
-        reduce_j(r, 0, w);
-        load_w(r, 1, w);
-        reduce_j(r, 1, w);
+        // (prefetching the weights under the K loop costs registers past the
+        // two-blocks-per-CU budget; an LDS-DMA prefetch and a reduction
+        // interleaved into the next a-block's MFMAs both measured slower)
+        load_w(r);
+        store_w(r);
+        __syncthreads();
+        reduce();
       }
     };
     if (nkt > 0) {
       if (wave_full) run1(std::false_type{});
       else           run1(std::true_type{});
     }
-    const int xg = (m0 >> 4) + wm * TM + q;
-    if (xg < p.fz.nx) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int g = n0 + wn * WN + j * 16 + r16;
-        if (g < p.N)
+    for (int u = 0; u < TQ; ++u) {
+      const int xg = (m0 >> 4) + wm * TM + 4 * u + q;
+      if (xg < p.fz.nx) {
 #pragma unroll
-          for (int c = 0; c < 3; ++c) p.fz.rho[(long)g * p.fz.rg + 3 * xg + c] = racc[j][c];
+        for (int j = 0; j < TN; ++j) {
+          const int g = n0 + wn * WN + j * 16 + r16;
+          if (g < p.N)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) p.fz.rho[(long)g * p.fz.rg + 3 * xg + c] = racc[u][j][c];
+        }
       }
     }
     return;
@@ -511,6 +560,7 @@ static const Cfg kCfg[] = {
   {64, 64, 32, 512, 2, 2},     // 4
   {128, 128, 16, 512, 2, 4},   // 5: C8 with BK 16, two blocks per CU
   {256, 128, 16, 256, 4, 2},   // 6: 256x128, 8 waves of 64x64, BK 16 (tuning only)
+  {128, 64, 16, 512, 2, 4},    // 7: 128x64, 8 waves of 64x16, BK 16, two blocks per CU
 };
 
 template <int BM, int BN, int WGM, int WGN, int BKT, int MINW, bool AK, bool BKc, int TAG, int MODE = 0>
@@ -692,7 +742,7 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
     p.ws = ws;
   }
   if (mode == 1) {
-    launch_one<128, 128, 2, 4, 32, 2, false, true, 4, 1>(p, st);
+    launch_one<128, 64, 2, 4, 16, 4, false, true, 4, 1>(p, st);
   } else if (mode == 2) {
     launch_one<128, 128, 2, 4, 32, 2, false, true, 5, 2>(p, st);
   } else switch (cfg) {
@@ -702,6 +752,7 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
     case 3: launch_cfg<64, 128, 2, 2, 32, 1>(p, st, akc, bkc, d.tag); break;
     case 5: launch_cfg<128, 128, 2, 4, 16, 4>(p, st, akc, bkc, d.tag); break;
     case 6: launch_cfg<256, 128, 4, 2, 16, 2>(p, st, akc, bkc, d.tag); break;
+    case 7: launch_cfg<128, 64, 2, 4, 16, 4>(p, st, akc, bkc, d.tag); break;
     default: launch_cfg<64, 64, 2, 2, 32, 2>(p, st, akc, bkc, d.tag); break;
   }
   if (p.nsplit > 1) {
