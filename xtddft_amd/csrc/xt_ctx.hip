@@ -910,8 +910,7 @@ static int xc_response(xt_ctx* c, int nz) {
       RET(gemm(c, b1));
       if (gga) {
         GemmDesc b2;   // accT[i][(xg,a)] += sum_g PhiO0[g][i] sum_c wv_c[g][xg] dPhiV_c[g][a]
-        const int nxb = (nzg + 7) / 8;
-        b2.M = O; b2.N = nxb * nab * 128; b2.K = n;
+        b2.M = O; b2.N = xc_m_cols(nzg, V); b2.K = n;
         b2.A = PO; b2.sAm = 1; b2.sAk = nmo;
         b2.fz.mode = 2; b2.fz.V = V; b2.fz.nx = nzg;
         b2.fz.w = PV + compP; b2.fz.wc = compP; b2.fz.wg = nmo;

@@ -81,7 +81,6 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINW)
 dgemm_kernel(GemmParams p) {
   static_assert(MODE == 0 || (BM == 128 && WGM * WGN == 8 && !A_KC && B_KC),
                 "fused XC modes run on 128-row 8-wave tiles, A MN-contiguous, B staged K-contiguous");
-  static_assert(MODE != 2 || BN == 128, "mode 2 staging map assumes a 128x128 tile");
   static_assert(MODE != 2 || (WGM == 2 && WGN == 4), "mode 2 staging map assumes 2x4 waves");
   constexpr int LDP = BK + 1;
   constexpr int NTHREADS = 64 * WGM * WGN;
@@ -134,8 +133,9 @@ dgemm_kernel(GemmParams p) {
 
   const int m0 = tm * BM, n0 = tn * BN;
   const int nkt = (p.K + BK - 1) / BK;
-  // mode 2: n-tile tn covers xg-block tn % nxb (8 xg) x a-block tn / nxb (16 a)
-  const int nxb = (p.fz.nx + 7) / 8;
+  // mode 2: n-tile tn covers xg-block tn % nxb (XGB = BN / 16 xg) x a-block tn / nxb (16 a)
+  constexpr int XGB = BN / 16;
+  const int nxb = (p.fz.nx + XGB - 1) / XGB;
   const int xg_blk = MODE == 2 ? tn % nxb : 0, a_blk = MODE == 2 ? tn / nxb : 0;
   const long units = (long)p.R * nkt;
   const long u_per = (units + p.nsplit - 1) / p.nsplit;
@@ -186,28 +186,36 @@ dgemm_kernel(GemmParams p) {
     }
   }
   a_row0 = (unsigned)(rowoff(min(m0 + a_fix, p.M - 1)) * 8);
-  // mode 2 staging map (BK = 32 k rows x 128 columns = 8 xg x 16 a): thread ->
-  // k row g2 = 4 wave + (tid >> 2 & 3), xg pair 2 p2 + {0,1} (p2 = tid >> 4 & 3), a quad
-  // 4 aq + {0..3} (aq = tid & 3): 6 rho + 12 gradient loads for 8 elements, each
-  // wave-load touching 4 grid rows, and the LDS stores of a 16-lane group land on
-  // 16 distinct bank pairs (4 rows x 4 quads, pitch 33).
-  const int g2 = (tid >> 6) * 4 + ((tid >> 2) & 3), p2 = (tid >> 4) & 3, aq2 = tid & 3;
-  int xg2[2], a2[4];
-  bool ok2[2][4];
+  // mode 2 staging maps: thread -> k row g2, NX xg (local xg_l) x NU a (local a_l)
+  //  BK 32 x BN 128 (8 xg x 16 a): g2 = 4 wave + (tid >> 2 & 3), xg_l = 2 (tid >> 4 & 3) + x,
+  //    a_l = 4 (tid & 3) + u: 6 rho + 12 gradient loads for 8 elements, each wave-load
+  //    touching 4 grid rows; the LDS stores of a 16-lane group land on 16 distinct
+  //    bank pairs (4 rows x 4 quads, pitch 33).
+  //  BK 16 x BN 64 (4 xg x 16 a): g2 = tid >> 5, xg_l = tid >> 3 & 3, a_l = 2 (tid & 7) + u:
+  //    3 rho + 6 gradient loads for 2 elements; stores of a 16-lane group hit
+  //    columns 2 ap + u + {0, 16} (pitch 17: distinct bank pairs).
+  static_assert(MODE != 2 || (BK == 32 && BN == 128 && NTHREADS == 512) ||
+                (BK == 16 && BN == 64 && NTHREADS == 512), "mode 2 staging map");
+  constexpr int NX = BN == 128 ? 2 : 1, NU = BN == 128 ? 4 : 2;
+  const int g2 = BN == 128 ? (tid >> 6) * 4 + ((tid >> 2) & 3) : tid >> 5;
+  auto xg_loc = [&](int x) XT_INLINE { return BN == 128 ? 2 * ((tid >> 4) & 3) + x : (tid >> 3) & 3; };
+  auto a_loc = [&](int u) XT_INLINE { return BN == 128 ? 4 * (tid & 3) + u : 2 * (tid & 7) + u; };
+  int xg2[NX], a2[NU];
+  bool ok2[NX][NU];
 #pragma unroll
-  for (int x = 0; x < 2; ++x) xg2[x] = xg_blk * 8 + 2 * p2 + x;
+  for (int x = 0; x < NX; ++x) xg2[x] = xg_blk * XGB + xg_loc(x);
 #pragma unroll
-  for (int u = 0; u < 4; ++u) a2[u] = a_blk * 16 + 4 * aq2 + u;
+  for (int u = 0; u < NU; ++u) a2[u] = a_blk * 16 + a_loc(u);
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int x = 0; x < NX; ++x)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) ok2[x][u] = xg2[x] < p.fz.nx && a2[u] < p.fz.V;
+    for (int u = 0; u < NU; ++u) ok2[x][u] = xg2[x] < p.fz.nx && a2[u] < p.fz.V;
 #pragma unroll
-  for (int x = 0; x < 2; ++x) xg2[x] = xg2[x] < p.fz.nx ? xg2[x] : p.fz.nx - 1;
+  for (int x = 0; x < NX; ++x) xg2[x] = xg2[x] < p.fz.nx ? xg2[x] : p.fz.nx - 1;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) a2[u] = a2[u] < p.fz.V ? a2[u] : p.fz.V - 1;
-  double bw[MODE == 2 ? 4 : 1][3];                 // mode 2: w_c[g][a_u]
-  double br[MODE == 2 ? 2 : 1][3];                 // mode 2: rho[g][xg_x][c]
+  for (int u = 0; u < NU; ++u) a2[u] = a2[u] < p.fz.V ? a2[u] : p.fz.V - 1;
+  double bw[MODE == 2 ? NU : 1][3];                // mode 2: w_c[g][a_u]
+  double br[MODE == 2 ? NX : 1][3];                // mode 2: rho[g][xg_x][c]
   b_row0 = (unsigned)((min(n0 + b_fix, p.N - 1) - n0) * 8);
 
   double ra[A_ELEMS], rb[B_ELEMS];
@@ -231,13 +239,13 @@ dgemm_kernel(GemmParams p) {
       // generated operand: raw inputs of k row g (clamped to the tile's first row past K)
       const long g = k0 + (g2 < kv ? g2 : 0);
 #pragma unroll
-      for (int x = 0; x < 2; ++x)
+      for (int x = 0; x < NX; ++x)
 #pragma unroll
         for (int c = 0; c < 3; ++c) br[x][c] = p.fz.rho[g * p.fz.rg + 3 * xg2[x] + c];
 #pragma unroll
       for (int c = 0; c < 3; ++c)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) bw[u][c] = p.fz.w[c * p.fz.wc + g * p.fz.wg + a2[u]];
+        for (int u = 0; u < NU; ++u) bw[u][c] = p.fz.w[c * p.fz.wc + g * p.fz.wg + a2[u]];
     } else {
 #pragma unroll
       for (int e = 0; e < B_ELEMS; ++e) {
@@ -258,10 +266,10 @@ dgemm_kernel(GemmParams p) {
     }
     if constexpr (MODE == 2) {
 #pragma unroll
-      for (int x = 0; x < 2; ++x)
+      for (int x = 0; x < NX; ++x)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int nn = (2 * p2 + x) * 16 + 4 * aq2 + u;
+        for (int u = 0; u < NU; ++u) {
+          const int nn = xg_loc(x) * 16 + a_loc(u);
           const double v = br[x][0] * bw[u][0] + br[x][1] * bw[u][1] + br[x][2] * bw[u][2];
           smem[buf * STAGE + BM * LDP + nn * LDP + g2] = (ok2[x][u] && g2 < kv) ? v : 0.0;
         }
@@ -486,7 +494,7 @@ dgemm_kernel(GemmParams p) {
   auto ccol = [&](int nl) XT_INLINE -> long {
     if (MODE != 2) return nl;
     const int c = nl - n0;
-    const int xg = xg_blk * 8 + c / 16, a = a_blk * 16 + (c & 15);
+    const int xg = xg_blk * XGB + c / 16, a = a_blk * 16 + (c & 15);
     return (xg < p.fz.nx && a < p.fz.V) ? (long)xg * p.fz.V + a : -1L;
   };
   if (p.nsplit > 1) {
@@ -532,8 +540,9 @@ __global__ void splitk_reduce(GemmParams p) {
     const int m = (int)(e / p.N), n = (int)(e % p.N);
     long cn = n;
     if (p.fz.mode == 2) {   // logical column -> xg V + a (see dgemm_kernel mode 2)
-      const int nxb = (p.fz.nx + 7) / 8, tn = n / 128, cc = n % 128;
-      const int xg = (tn % nxb) * 8 + cc / 16, a = (tn / nxb) * 16 + (cc & 15);
+      const int bn = XC_M_BN, xgb = bn / 16;
+      const int nxb = (p.fz.nx + xgb - 1) / xgb, tn = n / bn, cc = n % bn;
+      const int xg = (tn % nxb) * xgb + cc / 16, a = (tn / nxb) * 16 + (cc & 15);
       if (xg >= p.fz.nx || a >= p.fz.V) continue;
       cn = (long)xg * p.fz.V + a;
     }
@@ -552,7 +561,7 @@ __global__ void splitk_reduce(GemmParams p) {
 // block's barrier / prologue / epilogue hides under the other's MFMAs.
 // C4: 4 waves of 64x64.  Narrow tiles for small M or N.
 struct Cfg { int bm, bn, bk, slots, wgm, wgn; };
-static const Cfg kCfg[] = {
+static const Cfg kCfg[] = {   // (bm, bn, bk, concurrent block slots, wgm, wgn)
   {128, 128, 32, 256, 2, 4},   // 0: C8
   {128, 128, 16, 512, 2, 2},   // 1: C4
   {128, 64, 32, 256, 2, 2},    // 2
@@ -683,8 +692,8 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
   p.nbatch = (d.nb1 > 0 ? d.nb1 : 1) * p.nb2;
   p.ws = nullptr;
   p.fz = d.fz;
-  if (d.fz.mode != 0) {   // fused XC modes: fixed 128x128 8-wave BK 32 tile
-    const Cfg& c = kCfg[0];
+  if (d.fz.mode != 0) {   // fused XC modes: fixed tiles (mode 1 128x64, mode 2 XC_M_BN wide)
+    const Cfg& c = kCfg[7];
     const long units = (long)p.R * ((d.K + c.bk - 1) / c.bk);
     p.nsplit = d.fz.mode == 1 ? 1 : choose_split(c, d.M, d.N, p.nbatch, units);
     if (d.max_split > 0 && p.nsplit > d.max_split) p.nsplit = d.max_split;
@@ -700,6 +709,9 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
   else if (d.M >= 96) cfg = 2;
   else if (d.N >= 96) cfg = 3;
   else cfg = 4;
+  // the stored-exchange stream (skinny M, K = N = O V, HBM-bound): the 8-wave
+  // two-blocks-per-CU tile keeps more loads in flight than 64x128 (21.4 -> 20.0 ms)
+  if (d.tag == 1 && !ff && d.N >= 96) cfg = 5;
   if (forced_cfg() >= 0) cfg = forced_cfg();
   const Cfg& c = kCfg[cfg];
   const long units = (long)p.R * ((d.K + c.bk - 1) / c.bk);
@@ -715,7 +727,7 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
   if (mode != 0 && (d.sAm != 1 || d.fz.w == nullptr || d.fz.rho == nullptr || d.fz.nx <= 0 || d.fz.V <= 0))
     return XT_ERR_ARG;
   if (mode == 1 && (d.sBk != 1 || d.nb1 > 1 || d.nb2 > 1 || d.M != 16 * d.fz.nx)) return XT_ERR_ARG;
-  if (mode == 2 && (d.R > 1 || d.nb1 > 1 || d.nb2 > 1 || d.N % 128 != 0)) return XT_ERR_ARG;
+  if (mode == 2 && (d.R > 1 || d.nb1 > 1 || d.nb2 > 1 || d.N != xc_m_cols(d.fz.nx, d.fz.V))) return XT_ERR_ARG;
   const bool akc = mode == 0 && (d.sAk == 1);
   const bool bkc = mode != 0 || (d.sBk == 1);
   if (!akc && d.sAm != 1) return XT_ERR_ARG;
@@ -744,7 +756,8 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
   if (mode == 1) {
     launch_one<128, 64, 2, 4, 16, 4, false, true, 4, 1>(p, st);
   } else if (mode == 2) {
-    launch_one<128, 128, 2, 4, 32, 2, false, true, 5, 2>(p, st);
+    static_assert(XC_M_BN == 64, "mode 2 launch");
+    launch_one<128, 64, 2, 4, 16, 4, false, true, 5, 2>(p, st);
   } else switch (cfg) {
     case 0: launch_cfg<128, 128, 2, 4, 32, 2>(p, st, akc, bkc, d.tag); break;
     case 1: launch_cfg<128, 128, 2, 2, 16, 2>(p, st, akc, bkc, d.tag); break;

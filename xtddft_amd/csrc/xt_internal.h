@@ -18,7 +18,12 @@ namespace xt {
 //    A(r, m, k) = A[k sAk + xg ablk + 16 r + a_l]  (W = PhiO Zp, never stored);
 //    out: rho[g rg + 3 xg + c] = sum_a W[g, xg, a] w[c wc + g wg + a]   (c < 3)
 //  mode 2 "M backward":   B(g, n) generated as sum_c rho[g rg + 3 xg + c] w[c wc + g wg + a]
-//    with n -> (xg, a) in 8 x 16 blocks (xg-block fastest); C column xg V + a.
+//    with n -> (xg, a) in (XC_M_BN / 16) x 16 blocks (xg-block fastest); C column xg V + a;
+//    N must be xc_m_cols(nx, V).
+constexpr int XC_M_BN = 64;   // mode 2 column-tile width
+inline int xc_m_cols(int nx, int V) {
+  return ((nx + XC_M_BN / 16 - 1) / (XC_M_BN / 16)) * ((V + 15) / 16) * XC_M_BN;
+}
 struct XcFuse {
   int mode = 0;
   const double* w = nullptr;   // weights (grid gradients of the virtual MOs)
