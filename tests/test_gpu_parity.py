@@ -76,10 +76,11 @@ def test_xtda_utda(dev, xct, omega, kind, nz):
     assert rel(op.apply(z), vind(z)) < RTOL
 
 
-@pytest.mark.parametrize("nc,no", [(14, 2), (29, 3), (47, 2), (60, 1)])
+@pytest.mark.parametrize("nc,no", [(14, 2), (29, 3), (47, 2), (60, 1), (140, 2)])
 def test_xtda_many_occupied(dev, nc, no):
     """Occupied counts O = nc + no spanning 1..4 K-tiles of the fused XC kernels
-    (K = O there), with V not a multiple of their 16-wide virtual blocks."""
+    (K = O there) and the point kernel's register chunks (O > 128), with V not a
+    multiple of the 16-wide virtual blocks."""
     mf = make_mf(nao=nc + no + 53, nc=nc, no=no, xctype="GGA", hyb=0.2, ngrid=3000)
     vind, hdiag = oxtda.gen_tda_operation(mf)
     z = make_trial_vectors(9, hdiag.size)

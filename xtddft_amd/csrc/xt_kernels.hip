@@ -369,6 +369,152 @@ k_xc_uks_w(int g0, int ngrid, int nz, int O, int nmo, long compP,
   }
 }
 
+// Same contraction, one wave per grid point (4 per block), no LDS and no
+// block barrier: the point's occupied MO values / gradients live in registers
+// (IC chunks of 64 orbitals per lane), the 2NC partial sums of each x are reduced
+// by a transposing butterfly (halving steps hand each lane half of the values:
+// v_permlane32/16_swap for the cross-row steps, shuffles inside rows): 10
+// exchanges for the 8 GGA sums instead of 8 x 6, and lane l < 2NC computes
+// wv[l] from its own column of the kernel block.  HBM-bound on U / L.
+__device__ __forceinline__ void swap_rows32(double& A, double& B) {
+  const unsigned alo = (unsigned)__double2loint(A), ahi = (unsigned)__double2hiint(A);
+  const unsigned blo = (unsigned)__double2loint(B), bhi = (unsigned)__double2hiint(B);
+  const auto lo = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+  A = __hiloint2double((int)hi[0], (int)lo[0]);
+  B = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void swap_rows16(double& A, double& B) {
+  const unsigned alo = (unsigned)__double2loint(A), ahi = (unsigned)__double2hiint(A);
+  const unsigned blo = (unsigned)__double2loint(B), bhi = (unsigned)__double2hiint(B);
+  const auto lo = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+  A = __hiloint2double((int)hi[0], (int)lo[0]);
+  B = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+// Sum each of NV (power of two, <= 8) per-lane values over the wave; value j
+// ends in the lanes with lane >> (6 - log2 NV) == j.  Halving step at offset o:
+// the lower half (lane & o == 0) keeps index k, the upper k + n/2, each adding
+// its partner's copy (permlane swap of the pair (v[k], v[k + n/2]) leaves the
+// two copies of one index split across the two results in every lane).
+template <int NV>
+__device__ __forceinline__ double wave_sum_transpose(double (&v)[NV], int lane) {
+  static_assert(NV == 1 || NV == 2 || NV == 4 || NV == 8, "NV");
+  int n = NV;
+  if constexpr (NV >= 2) {
+#pragma unroll
+    for (int k = 0; k < NV / 2; ++k) { swap_rows32(v[k], v[k + NV / 2]); v[k] += v[k + NV / 2]; }
+    n = NV / 2;
+  }
+  if constexpr (NV >= 4) {
+#pragma unroll
+    for (int k = 0; k < NV / 4; ++k) { swap_rows16(v[k], v[k + NV / 4]); v[k] += v[k + NV / 4]; }
+    n = NV / 4;
+  }
+  if constexpr (NV >= 8) {   // offset 8 inside a row: explicit keep / send
+    const bool up = lane & 8;
+    const double send = up ? v[0] : v[1];
+    const double keep = up ? v[1] : v[0];
+    v[0] = keep + __shfl_xor(send, 8);
+  }
+  (void)n;
+  double t = v[0];
+#pragma unroll
+  for (int o = 32 / NV; o > 0; o >>= 1) t += __shfl_xor(t, o);
+  return t;
+}
+
+template <int NC, int IC>
+__global__ void __launch_bounds__(256)
+k_xc_point(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
+           const double* __restrict__ pO0, const double* __restrict__ pO1,
+           const double* __restrict__ wfxc,
+           double* __restrict__ U0, long ldU0, double* __restrict__ U1, long ldU1,
+           double* __restrict__ R0, long ldR0, double* __restrict__ R1, long ldR1) {
+  constexpr int NV = 2 * NC;
+  constexpr int SH = NV == 8 ? 3 : (NV == 2 ? 5 : 4);   // value j lives at lanes j << SH
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= G) return;   // whole waves only; no block-level synchronisation below
+  const long gg = g0 + g;
+  double ph[2][NC][IC];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const double* po = s ? pO1 : pO0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int m = 0; m < IC; ++m) {
+        const int i = lane + 64 * m;
+        ph[s][c][m] = i < O ? po[c * compP + gg * nmo + i] : 0.0;
+      }
+  }
+  // lane l < NV: column (s, y) = (l / NC, l % NC) of the (w fxc) block at this point
+  const int sl = lane / NC, yl = lane % NC;
+  double fk[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int t = k / NC, yy = k % NC;
+    fk[k] = lane < NV ? wfxc[(long)(((t * NC + yy) * 2 + sl) * NC + yl) * ngrid + gg] : 0.0;
+  }
+  double* Ub[2] = {U0 + g * ldU0, U1 + g * ldU1};
+  double* Rb[2] = {R0 ? R0 + g * ldR0 : nullptr, R1 ? R1 + g * ldR1 : nullptr};
+  for (int x = 0; x < nz; ++x) {
+    double v[NV];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      double u[IC];
+#pragma unroll
+      for (int m = 0; m < IC; ++m) {
+        const int i = lane + 64 * m;
+        u[m] = i < O ? Ub[s][(long)x * O + i] : 0.0;
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        double a = 0.0;
+#pragma unroll
+        for (int m = 0; m < IC; ++m) a += u[m] * ph[s][c][m];
+        v[s * NC + c] = a;
+      }
+    }
+    const double tot = wave_sum_transpose<NV>(v, lane);
+    double rho[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) rho[j] = readlane_d(tot, j << SH);
+    if constexpr (NC > 1) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int c = 1; c < NC; ++c) rho[s * NC + c] += Rb[s][3 * x + c - 1];
+    }
+    double wl = 0.0;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) wl += fk[k] * rho[k];
+    double wv[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) wv[j] = readlane_d(wl, j);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int m = 0; m < IC; ++m) {
+        const int i = lane + 64 * m;
+        double l = 0.0;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) l += wv[s * NC + c] * ph[s][c][m];
+        if (i < O) Ub[s][(long)x * O + i] = l;
+      }
+    if constexpr (NC > 1) {
+      if (lane < NV && yl > 0) Rb[sl][3 * x + yl - 1] = wl;
+    }
+  }
+}
+
 // ALDA0 spin-flip kernel (SF_TDA.py:90-160): rho1 = sum_i U0 PhiO, wv = rho1*fsf, S0 = wv*PhiO
 __global__ void __launch_bounds__(256)
 k_xc_sf(int G, int g0, int nz, int O, int nmo, const double* __restrict__ phio,
@@ -550,6 +696,15 @@ void xc_uks(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, 
 void xc_uks_w(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
               const double* pO0, const double* pO1, const double* wfxc, double* U0, long ldU0,
               double* U1, long ldU1, double* R0, long ldR0, double* R1, long ldR1) {
+  if (O <= 256) {   // one wave per grid point, occupied values in registers
+    const dim3 grid((G + 3) / 4), blk(256);
+#define XT_POINT(NC, IC) hipLaunchKernelGGL((k_xc_point<NC, IC>), grid, blk, 0, st, G, g0, ngrid, nz, O, nmo, compP, \
+                                            pO0, pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1)
+    if (ncomp == 4) { if (O <= 128) XT_POINT(4, 2); else XT_POINT(4, 4); }
+    else            { if (O <= 128) XT_POINT(1, 2); else XT_POINT(1, 4); }
+#undef XT_POINT
+    return;
+  }
   const bool same = (pO0 == pO1);
   const size_t lds = (same ? 1 : 2) * (size_t)ncomp * O * sizeof(double);
   if (ncomp == 4)
