@@ -61,6 +61,27 @@ def test_xtda_on_roks_molecule_matches_oracle(torch):
     e = x.kernel()
     assert np.all(x.converged)
     assert np.abs(np.asarray(e) - w).max() < 1e-7
+    # length-form oscillator strengths (XTDA.py:838-858) from the device eigenvectors
+    # against the same formula on the oracle's explicit-A eigenvectors, summed over
+    # degenerate groups (Pi pairs of the C2v molecule mix freely)
+    f = x.osc_str()
+    A = vind(np.eye(hdiag.size)).T
+    we, ve = np.linalg.eigh(A)
+    keep = we > 1e-3
+    we, ve = we[keep][:6], ve[:, keep][:, :6]
+    mol, c = mf.extra["qc_mol"], mf.mo_coeff
+    dip = mol.intor_symmetric("int1e_r", comp=3)
+    occ_a, vir_a = mf.mo_occ >= 1, mf.mo_occ == 0
+    occ_b, vir_b = mf.mo_occ >= 2, mf.mo_occ != 2
+    da = np.einsum('xpq,pi,qj->xij', dip, c[:, occ_a], c[:, vir_a]).reshape(3, -1)
+    db = np.einsum('xpq,pi,qj->xij', dip, c[:, occ_b], c[:, vir_b]).reshape(3, -1)
+    td = ve[:da.shape[1]].T @ da.T + ve[da.shape[1]:].T @ db.T     # PySCF vector order
+    f_ref = 2.0 / 3.0 * we * np.einsum('sx,sx->s', td, td)
+    groups = np.cumsum(np.r_[0, np.diff(we) > 1e-6])
+    for gidx in np.unique(groups)[:-1]:     # the last group may be cut by nstates
+        sel = groups == gidx
+        # eigenvectors converge to the residual tolerance 1e-5 (XTDA.py:775): f to ~1e-5 relative
+        assert abs(f[sel].sum() - f_ref[sel].sum()) <= 1e-5 * max(f_ref[sel].sum(), 1e-6)
 
 
 def test_sf_up_on_aufbau_triplet_matches_oracle(torch):

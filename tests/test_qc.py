@@ -76,6 +76,12 @@ def test_spd_one_electron_integrals_against_grid_quadrature():
     t_grid = 0.5 * np.einsum('g,xgp,xgq->pq', w, ao[1:], ao[1:])
     assert np.abs(s_grid - mol.intor("int1e_ovlp")).max() < 1e-6
     assert np.abs(t_grid - mol.intor("int1e_kin")).max() < 1e-5
+    # dipole integrals (osc_str, XTDA.py:850): <p| r - O |q> by quadrature, two origins
+    for origin in ((0.0, 0.0, 0.0), (0.4, -0.3, 1.2)):
+        r_grid = np.einsum('g,gp,gq,gd->dpq', w, ao[0], ao[0], g.coords - np.asarray(origin))
+        r_ana = mol.intor_symmetric("int1e_r", comp=3, origin=origin)
+        assert r_ana.shape == (3, mol.nao, mol.nao)
+        assert np.abs(r_grid - r_ana).max() < 1e-5
 
 
 def test_grid_pruning_and_size_match_reference():

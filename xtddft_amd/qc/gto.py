@@ -226,8 +226,12 @@ class Mole:
             out = out * (nrm[:, None] * nrm[None, :])
         return out
 
-    def intor(self, name: str, origin=(0.0, 0.0, 0.0)):
-        """PySCF names: int1e_ovlp, int1e_kin, int1e_nuc, int1e_r, int2e."""
+    def intor_symmetric(self, name: str, comp=None, origin=(0.0, 0.0, 0.0)):
+        """PySCF ``Mole.intor_symmetric`` (the one-electron integrals here are all hermitian)."""
+        return self.intor(name, comp=comp, origin=origin)
+
+    def intor(self, name: str, comp=None, hermi=0, origin=(0.0, 0.0, 0.0)):
+        """PySCF names: int1e_ovlp, int1e_kin, int1e_nuc, int1e_r (comp 3), int2e."""
         key = name.replace("_sph", "")
         if key == "int1e_ovlp":
             return self._intor_raw("ovlp")

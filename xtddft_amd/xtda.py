@@ -182,9 +182,15 @@ class XTDA:
                 + np.einsum('ij,ij->i', self.xycv_b, self.xycv_b)
                 - 2 * np.einsum('ij,ij->i', self.xycv_a, self.xycv_b))
 
-    def osc_str(self, dipole_ao):
-        """Length-form oscillator strengths (XTDA.py:838-858) for given AO dipole
-        integrals (3, nao, nao) -- the integral itself is not part of the hot path."""
+    def osc_str(self, dipole_ao=None):
+        """Length-form oscillator strengths (XTDA.py:838-858).  ``dipole_ao``
+        (3, nao, nao) defaults to ``mol.intor_symmetric('int1e_r', comp=3)`` (the
+        reference's call, origin 0) when ``mol`` provides integrals."""
+        if dipole_ao is None:
+            mol = self.mol if hasattr(self.mol, "intor_symmetric") else self.mf.extra.get("qc_mol")
+            if mol is None or not hasattr(mol, "intor_symmetric"):
+                raise ValueError("osc_str needs AO dipole integrals: pass dipole_ao or a Mole with intor")
+            dipole_ao = mol.intor_symmetric("int1e_r", comp=3)
         mf = self.mf
         c = mf.mo_coeff
         occ_a = mf.mo_occ >= 1
