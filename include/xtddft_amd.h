@@ -142,9 +142,11 @@ int xt_dim(const xt_ctx* ctx);
 /* per-phase device timings of the last xt_apply (ms): jk, xc, local, total */
 int xt_last_timings(const xt_ctx* ctx, double* out4);
 
-/* live timing of GEMM classes (mask bit t: t = 1 DF exchange contraction, 2 XC grid
-   forward, 3 XC back-projection; 0 = off); xt_profile_stats(tag): {device ms summed over the
-   launches of the last xt_apply, number of launches, algorithmic flops} */
+/* live timing of GEMM classes with HIP events on the context's stream (mask bit t:
+   t = 1 exchange contraction (stored or direct), 2 XC forward U, 3 XC back L,
+   4 XC forward W (fused rho), 5 XC back M (fused generated operand); 0 = off);
+   xt_profile_stats(tag): {device ms summed over the launches of the last xt_apply,
+   number of launches, algorithmic flops} */
 int xt_set_profile(xt_ctx* ctx, int tag);
 int xt_profile_stats(const xt_ctx* ctx, int tag, double* out3);
 
