@@ -160,7 +160,6 @@ dgemm_kernel(GemmParams p) {
   const int a_fix = A_KC ? tid % BK : tid % BM, a_var = A_KC ? tid / BK : tid / BM;
   const int b_fix = B_KC ? tid % BK : tid % BN, b_var = B_KC ? tid / BK : tid / BN;
   unsigned aoff[A_ELEMS], boff[B_ELEMS];
-  unsigned a_row0, b_row0;   // MN-contiguous operands: offset of k-row 0 (k-edge fallback)
   // mode 1 rows m = 16 xg + a_l sit at xg * ablk + a_l (the a-block via r * sAr)
   auto rowoff = [&](int mg) XT_INLINE -> long {
     return MODE == 1 ? (long)(mg >> 4) * p.fz.ablk + (mg & 15) : (long)(mg - m0);
@@ -185,7 +184,6 @@ dgemm_kernel(GemmParams p) {
       boff[e] = (unsigned)(((long)(b_var + e * B_STEP) * p.sBk + nn) * 8);
     }
   }
-  a_row0 = (unsigned)(rowoff(min(m0 + a_fix, p.M - 1)) * 8);
   // mode 2 staging maps: thread -> k row g2, NX xg (local xg_l) x NU a (local a_l)
   //  BK 32 x BN 128 (8 xg x 16 a): g2 = 4 wave + (tid >> 2 & 3), xg_l = 2 (tid >> 4 & 3) + x,
   //    a_l = 4 (tid & 3) + u: 6 rho + 12 gradient loads for 8 elements, each wave-load
@@ -216,7 +214,6 @@ dgemm_kernel(GemmParams p) {
   for (int u = 0; u < NU; ++u) a2[u] = a2[u] < p.fz.V ? a2[u] : p.fz.V - 1;
   double bw[MODE == 2 ? NU : 1][3];                // mode 2: w_c[g][a_u]
   double br[MODE == 2 ? NX : 1][3];                // mode 2: rho[g][xg_x][c]
-  b_row0 = (unsigned)((min(n0 + b_fix, p.N - 1) - n0) * 8);
 
   double ra[A_ELEMS], rb[B_ELEMS];
 
@@ -232,7 +229,7 @@ dgemm_kernel(GemmParams p) {
     for (int e = 0; e < A_ELEMS; ++e) {
       unsigned o;
       if (A_KC) o = (a_fix < kv) ? aoff[e] : aoff[e] - (unsigned)(a_fix * 8);
-      else      o = (a_var + e * A_STEP < kv) ? aoff[e] : a_row0;
+      else      o = (a_var + e * A_STEP < kv) ? aoff[e] : aoff[e] - (unsigned)((a_var + e * A_STEP) * p.sAk * 8);
       ra[e] = *(const double*)(At + o);
     }
     if constexpr (MODE == 2) {
@@ -251,7 +248,7 @@ dgemm_kernel(GemmParams p) {
       for (int e = 0; e < B_ELEMS; ++e) {
         unsigned o;
         if (B_KC) o = (b_fix < kv) ? boff[e] : boff[e] - (unsigned)(b_fix * 8);
-        else      o = (b_var + e * B_STEP < kv) ? boff[e] : b_row0;
+        else      o = (b_var + e * B_STEP < kv) ? boff[e] : boff[e] - (unsigned)((b_var + e * B_STEP) * p.sBk * 8);
         rb[e] = *(const double*)(Bt + o);
       }
     }
@@ -701,11 +698,11 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
     return;
   }
   int cfg;
-  // 128x128: two 8-wave blocks per CU (BK 16, 128-register budget) except for
-  // the (m-contiguous A, n-contiguous B) layout, which spills there and runs
-  // one 8-wave block per CU with BK 32 (measured, tools/gemm_bench.py)
+  // 128x128: two 8-wave blocks per CU (BK 16, 128-register budget) for every
+  // layout (the k-edge fallback offsets are recomputed per load so the
+  // (m-contiguous A, n-contiguous B) layout fits too: XC back L 151 -> 150 ms)
   const bool ff = (d.sAk != 1) && (d.sBk != 1);
-  if (d.M >= 96 && d.N >= 96) cfg = ff ? 0 : 5;
+  if (d.M >= 96 && d.N >= 96) cfg = 5;
   else if (d.M >= 96) cfg = 2;
   else if (d.N >= 96) cfg = 3;
   else cfg = 4;
