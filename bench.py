@@ -282,10 +282,17 @@ def main():
         hdiag = x._hdiag()
         x0 = x.get_init_guess(mf, args.nroots)
 
+        aop_stats = dict(calls=0, vectors=0, s=0.0)
+
         def aop(xt):
+            t = time.perf_counter()
             s = op.apply(xt)
             if world > 1:
                 dist.all_reduce(s)
+            torch.cuda.synchronize()
+            aop_stats["calls"] += 1
+            aop_stats["vectors"] += int(s.shape[0])
+            aop_stats["s"] += time.perf_counter() - t
             return s
 
         def pickeig(w, v, nroots, envs):
@@ -301,6 +308,7 @@ def main():
         result["converge"] = dict(nroots=args.nroots, wall_s=round(wall, 2),
                                   wall_s_incl_exchange_build=round(wall + op.prepare_s, 2),
                                   iterations=int(icyc) + 1, converged=bool(np.all(conv)),
+                                  ax_vectors=aop_stats["vectors"], ax_s=round(aop_stats["s"], 2),
                                   e_min_ha=float(e[0]), criteria="|de|<1e-12, |r|<1e-5 (XTDA.py:775)")
     if rank == 0:
         print(json.dumps(result), flush=True)
