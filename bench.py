@@ -39,6 +39,10 @@ FP64_PEAK_TFLOPS = 78.6     # MI355X dense FP64 matrix peak (AMD spec); 74.2 mea
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+KIND_NAME = {"XTDA": "X-TDA", "SF_UP": "SF-TDA (spin-flip up)", "SF_DOWN": "SF-TDA (spin-flip down)",
+             "XSF": "XSF-TDA"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -58,7 +62,29 @@ def parse():
     ap.add_argument("--nroots", type=int, default=20)
     ap.add_argument("--k-mode", default="auto", choices=["auto", "direct", "stored"],
                     help="exchange evaluation (xt_set_exchange_mode)")
-    return ap.parse_args()
+    ap.add_argument("--kind", default="XTDA", choices=["XTDA", "SF_UP", "SF_DOWN", "XSF"],
+                    help="operator (XTDA.py / SF_TDA.py / XSF_TDA.py vind)")
+    ap.add_argument("--sa", type=int, default=0, help="XSF spin-adaptation level (XSF_TDA.py SA)")
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="BASELINE.json shape preset (synthetic data of that shape); the default "
+                         "bench line is the headline H")
+    args = ap.parse_args()
+    if args.config:
+        for k, v in CONFIGS[args.config].items():
+            setattr(args, k, v)
+    return args
+
+
+# BASELINE.json configs as synthetic shapes (SURVEY.md 8 shape table): nao, closed /
+# open shells, operator, vectors per A.x (= nroots), hybrid fraction.  C4 is the
+# XSF doublet, run at SA = 0 (SA > 0 divides by 2S - 1 = 0, XSF_TDA.py:1102-1121).
+CONFIGS = {
+    "H": dict(nao=1000, nc=99, no=2, kind="XTDA", nvec=20, nroots=20, hyb=0.2),
+    "C2": dict(nao=180, nc=33, no=1, kind="XTDA", nvec=20, nroots=20, hyb=0.2),
+    "C3": dict(nao=861, nc=91, no=4, kind="SF_UP", nvec=30, nroots=30, hyb=0.5),
+    "C4": dict(nao=840, nc=180, no=1, kind="XSF", nvec=40, nroots=40, hyb=0.5, sa=0),
+    "C5": dict(nao=152, nc=35, no=2, kind="XTDA", nvec=50, nroots=50, hyb=0.2),
+}
 
 
 def cpu_baseline(args):
@@ -174,7 +200,11 @@ def main():
     mf = make_device_mf(nao=args.nao, nc=args.nc, no=args.no, naux=naux, ngrid=ngrid,
                         xctype=args.xc, hyb=args.hyb, device=local, shard=(rank, world),
                         full_aux=replicate)
-    op = DeviceOperator(mf, "XTDA", shard=(rank, world), device=local,
+    kw = {}
+    if args.kind == "XSF":
+        # XSF_TDA.kernel default fglobal = (1 - d_lda) c_x + d_lda, d_lda = 0.3, c_x = hyb
+        kw = dict(sa=args.sa, fglobal=0.7 * args.hyb + 0.3, foo=1.0, remove=False)
+    op = DeviceOperator(mf, args.kind, shard=(rank, world), device=local, **kw,
                         presharded="grid" if replicate else True, k_mode=args.k_mode,
                         replicate_df=replicate)
     mf.cderi = None
@@ -228,8 +258,10 @@ def main():
     traffic = load_traffic(dom_name)
     if dom_name == "mo_exchange_stored":
         # HBM-bound: streams the stored exchange matrix once per launch (+ Ze in, sigma in/out)
-        ov = (args.nc + args.no) * (args.no + nv)
-        nzg = 2 * args.nvec
+        occ = args.nc if args.kind == "SF_UP" else args.nc + args.no
+        vir = nv if args.kind == "SF_UP" else args.no + nv
+        ov = occ * vir
+        nzg = (2 if args.kind == "XTDA" else 1) * args.nvec
         bytes_launch = 8.0 * (ov * ov + 3.0 * nzg * ov)
         gbs = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         roofline = dict(bound="hbm", achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s",
@@ -253,9 +285,11 @@ def main():
         ms_per_step=round(1e3 * T / args.steps, 3),
         higher_is_better=True, scaling="strong", vs_baseline=None, dtype="f64",
         data="synthetic (seeded ROKS mean field, DF factor, GGA grid kernel; generated in HBM)",
-        config=dict(workload=(f"X-TDA A.x, nao={args.nao}, nocc_a/nocc_b={args.nc + args.no}/{args.nc}, "
-                              f"nocc*nvir={(args.nc + args.no) * nv}+{args.nc * (args.no + nv)}, "
-                              f"nvec={args.nvec}, naux={naux}, ngrid={ngrid}, xc={args.xc}, hyb={args.hyb}"),
+        config=dict(workload=(f"{KIND_NAME[args.kind]} A.x, nao={args.nao}, nocc_a/nocc_b={args.nc + args.no}/{args.nc}, "
+                              f"dim={op.dim}, "
+                              f"nvec={args.nvec}, naux={naux}, ngrid={ngrid}, xc={args.xc}, hyb={args.hyb}"
+                              + (f", SA={args.sa}" if args.kind == "XSF" else "")
+                              + (f" [BASELINE {args.config}]" if args.config else "")),
                     nao=args.nao, dim=op.dim, nvec=args.nvec, naux=naux, ngrid=ngrid,
                     parallelism=(f"grid sharded x{world}; " +
                                  ("replicated MO DF factor, aux window + stored-exchange rows"
@@ -268,13 +302,13 @@ def main():
         exchange=dict(mode=op.k_mode, stored_gib=round(op.k_gib, 2), build_s=round(op.prepare_s, 3)),
     )
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.kind == "XTDA":
         try:
             result["cpu_baseline"] = cpu_baseline(args)
         except Exception as e:   # report, never hide
             result["cpu_baseline"] = dict(value=None, error=repr(e))
 
-    if (world == 1 and not args.no_converge) or args.converge:
+    if ((world == 1 and not args.no_converge) or args.converge) and args.kind == "XTDA":
         from xtddft_amd.davidson import DiagPrecond, davidson1
         from xtddft_amd.xtda import XTDA
         x = XTDA.__new__(XTDA)

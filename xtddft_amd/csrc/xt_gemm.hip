@@ -79,8 +79,9 @@ __device__ __forceinline__ double rows_sum4(double v) {
 template <int BM, int BN, int WGM, int WGN, int BK, int MINW, bool A_KC, bool B_KC, int TAG, int MODE = 0>
 __global__ void __launch_bounds__(64 * WGM * WGN, MINW)
 dgemm_kernel(GemmParams p) {
-  static_assert(MODE == 0 || (BM == 128 && WGM * WGN == 8 && !A_KC && B_KC),
-                "fused XC modes run on 128-row 8-wave tiles, A MN-contiguous, B staged K-contiguous");
+  static_assert(MODE == 0 || ((BM == 128 || (MODE == 2 && BM == 64)) && WGM * WGN == 8 && !A_KC && B_KC),
+                "fused XC modes run on 128-row (mode 2 also 64-row) 8-wave tiles, A MN-contiguous, "
+                "B staged K-contiguous");
   static_assert(MODE != 2 || (WGM == 2 && WGN == 4), "mode 2 staging map assumes 2x4 waves");
   constexpr int LDP = BK + 1;
   constexpr int NTHREADS = 64 * WGM * WGN;
@@ -754,7 +755,9 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
     launch_one<128, 64, 2, 4, 16, 4, false, true, 4, 1>(p, st);
   } else if (mode == 2) {
     static_assert(XC_M_BN == 64, "mode 2 launch");
-    launch_one<128, 64, 2, 4, 16, 4, false, true, 5, 2>(p, st);
+    // rows = occupied orbitals: a 64-row tile when they fit (small molecules)
+    if (d.M <= 64) launch_one<64, 64, 2, 4, 16, 4, false, true, 5, 2>(p, st);
+    else           launch_one<128, 64, 2, 4, 16, 4, false, true, 5, 2>(p, st);
   } else switch (cfg) {
     case 0: launch_cfg<128, 128, 2, 4, 32, 2>(p, st, akc, bkc, d.tag); break;
     case 1: launch_cfg<128, 128, 2, 2, 16, 2>(p, st, akc, bkc, d.tag); break;
