@@ -92,3 +92,32 @@ def test_sf_up_on_aufbau_triplet_matches_oracle(torch):
     w = np.linalg.eigvalsh(vind(np.eye(hdiag.size)).T)[:5]
     e_ev, _ = SF_TDA(mf, isf=1).kernel(nstates=5)
     assert np.abs(np.asarray(e_ev) / HA2EV - w).max() < 1e-7
+
+
+def test_rotatory_strengths_of_mirror_images(torch):
+    """XTDA rotatory strengths (XTDA.py:860-891) on a chiral open-shell molecule
+    (twisted H2F2 triplet, 6-31G, ROKS BHandHLYP): the mirror image has the same
+    excitation energies and oscillator strengths and opposite rotatory strengths.
+    (The reference prints rot_str only for chiral molecules and stores none for a
+    basis available offline: checked by this symmetry and the quadrature-tested
+    integrals, test_qc.py.)"""
+    from xtddft_amd import XTDA
+    from xtddft_amd.qc import M, ROKS
+    out = []
+    for s in (1.0, -1.0):
+        geom = f"F 0 0 0; F 0 0 {1.42 * s}; H 0.92 0 {-0.25 * s}; H 0.46 0.80 {1.67 * s}"
+        mol = M(geom, basis="6-31G", spin=2)
+        mf = ROKS(mol, "bhandhlyp")
+        mf.conv_tol = 1e-10
+        mf.kernel()
+        assert mf.converged
+        x = XTDA(mol, mf.to_meanfield(), nstates=4)
+        e = np.asarray(x.kernel())
+        _, f, r = x.properties()
+        out.append((e, np.asarray(f), np.asarray(r)))
+    (e1, f1, r1), (e2, f2, r2) = out
+    assert np.abs(e1 - e2).max() < 1e-7
+    assert np.abs(f1 - f2).max() <= 1e-5 * max(f1.max(), 1e-6)
+    scale = np.abs(r1).max()
+    assert scale > 1e-6
+    assert np.abs(r1 + r2).max() <= 1e-4 * scale

@@ -82,6 +82,18 @@ def test_spd_one_electron_integrals_against_grid_quadrature():
         r_ana = mol.intor_symmetric("int1e_r", comp=3, origin=origin)
         assert r_ana.shape == (3, mol.nao, mol.nao)
         assert np.abs(r_grid - r_ana).max() < 1e-5
+    # rotatory-strength integrals (XTDA.py:870,873): <nabla p|q> and <p|(r - O) x nabla|q>
+    ip_grid = np.einsum('g,xgp,gq->xpq', w, ao[1:], ao[0])
+    assert np.abs(ip_grid - mol.intor("int1e_ipovlp", comp=3, hermi=2)).max() < 1e-5
+    for origin in ((0.0, 0.0, 0.0), (0.4, -0.3, 1.2)):
+        d = (g.coords - np.asarray(origin))[:, :, None]
+        lz = np.stack([d[:, 1] * ao[3] - d[:, 2] * ao[2],      # (r x nabla)_x
+                       d[:, 2] * ao[1] - d[:, 0] * ao[3],
+                       d[:, 0] * ao[2] - d[:, 1] * ao[1]])
+        l_grid = np.einsum('g,gp,xgq->xpq', w, ao[0], lz)
+        l_ana = mol.intor("int1e_cg_irxp", comp=3, hermi=2, origin=origin)
+        assert np.abs(l_grid - l_ana).max() < 1e-5
+        assert np.abs(l_ana + l_ana.transpose(0, 2, 1)).max() < 1e-12
 
 
 def test_grid_pruning_and_size_match_reference():
@@ -152,3 +164,33 @@ def test_usf_delta_s2_matches_reference():
     ds = [delta_s2_u(mfd, v[:, n], o.nc, o.no, o.nv) - o.no + 1 for n in range(10)]
     ref = reference_outputs()["usf_uks_alda0_delta_s2"]
     assert np.abs(np.asarray(ds) - ref).max() < 1e-5
+
+
+def test_chiral_mol():
+    """gto.mole.chiral_mol (XTDA.py:818): mirror-image superposition test."""
+    from xtddft_amd.qc.gto import chiral_mol
+
+    class Geo:
+        def __init__(self, x, z):
+            self.x, self.z = np.asarray(x, float), np.asarray(z, float)
+
+        def atom_coords(self):
+            return self.x
+
+        def atom_charges(self):
+            return self.z
+    t = np.array([[1, 1, 1], [1, -1, -1], [-1, 1, -1], [-1, -1, 1]], float)
+    q, _ = np.linalg.qr(np.random.default_rng(1).standard_normal((3, 3)))
+    if np.linalg.det(q) < 0:
+        q[:, 0] *= -1
+    cent = np.vstack([[0, 0, 0], t])
+    assert chiral_mol(Geo(cent @ q.T + 0.3, [6, 1, 9, 17, 35]))           # CHFClBr
+    assert chiral_mol(Geo(cent * [1, 1, -1], [6, 1, 9, 17, 35]))          # its mirror image
+    assert not chiral_mol(Geo(cent @ q.T, [6, 1, 1, 17, 35]))              # CH2ClBr (Cs)
+    assert not chiral_mol(Geo(t, [1, 1, 1, 1]))                            # Td
+    assert not chiral_mol(Geo([[0, 0, 0.5], [1, 0, 0], [-0.5, 0.866, 0], [-0.5, -0.866, 0]],
+                              [9, 1, 1, 1]))                               # C3v
+    assert not chiral_mol(Geo([[0, 0, 0], [1, 0, 0], [0, 1, 0], [1, 1.2, 0]], [1, 1, 9, 1]))  # planar
+    twisted = [[1, 0, 0], [0, 0, 0], [0, 0, 1.5], [0.5, 0.866, 1.5]]         # H-F-F-H, 60 deg
+    assert chiral_mol(Geo(twisted, [1, 9, 9, 1]))
+    assert not chiral_mol(Geo([[1, 0, 0], [0, 0, 0], [0, 0, 1.5], [-1, 0, 1.5]], [1, 9, 9, 1]))  # trans

@@ -191,7 +191,7 @@ class Mole:
     # ----------------------------------------------------------- integrals
     def _intor_raw(self, kind, origin=(0.0, 0.0, 0.0)):
         n = self._nao
-        if kind == "r":
+        if kind in ("r", "ipovlp", "irxp"):
             out = np.zeros((3, n, n))
         else:
             out = np.zeros((n, n))
@@ -201,7 +201,7 @@ class Mole:
             for j in range(i + 1):
                 sj = sh[j]
                 Tj = _sph_transform(sj.l)
-                pair = ShellPair(si, sj, kin=(kind == "kin"))
+                pair = ShellPair(si, sj, kin=kind in ("kin", "ipovlp", "irxp"))
                 if kind == "ovlp":
                     blk = pair.overlap()
                 elif kind == "kin":
@@ -210,14 +210,20 @@ class Mole:
                     blk = pair.nuclear(self._charges, self._coords)
                 elif kind == "r":
                     blk = pair.multipole1(np.asarray(origin, dtype=np.float64))
+                elif kind == "ipovlp":     # <nabla a | b> = -<a | nabla b>
+                    blk = -pair.deriv1()
+                elif kind == "irxp":       # <a | (r - O) x nabla | b>
+                    blk = pair.angmom(np.asarray(origin, dtype=np.float64))
                 else:
                     raise KeyError(kind)
-                blk = Ti @ blk @ Tj.T if kind != "r" else np.einsum('mi,dij,nj->dmn', Ti, blk, Tj)
+                three = kind in ("r", "ipovlp", "irxp")
+                blk = np.einsum('mi,dij,nj->dmn', Ti, blk, Tj) if three else Ti @ blk @ Tj.T
                 a0, a1 = self.ao_loc[i], self.ao_loc[i + 1]
                 b0, b1 = self.ao_loc[j], self.ao_loc[j + 1]
-                if kind == "r":
+                if three:
+                    sign = 1.0 if kind == "r" else -1.0   # hermitian / anti-hermitian
+                    out[:, b0:b1, a0:a1] = sign * blk.transpose(0, 2, 1)
                     out[:, a0:a1, b0:b1] = blk
-                    out[:, b0:b1, a0:a1] = blk.transpose(0, 2, 1)
                 else:
                     out[a0:a1, b0:b1] = blk
                     out[b0:b1, a0:a1] = blk.T
@@ -231,7 +237,8 @@ class Mole:
         return self.intor(name, comp=comp, origin=origin)
 
     def intor(self, name: str, comp=None, hermi=0, origin=(0.0, 0.0, 0.0)):
-        """PySCF names: int1e_ovlp, int1e_kin, int1e_nuc, int1e_r (comp 3), int2e."""
+        """PySCF names: int1e_ovlp, int1e_kin, int1e_nuc, int1e_r, int1e_ipovlp,
+        int1e_cg_irxp (comp 3; common gauge origin = ``origin``, PySCF's default 0), int2e."""
         key = name.replace("_sph", "")
         if key == "int1e_ovlp":
             return self._intor_raw("ovlp")
@@ -241,6 +248,10 @@ class Mole:
             return self._intor_raw("nuc")
         if key == "int1e_r":
             return self._intor_raw("r", origin)
+        if key == "int1e_ipovlp":       # (nabla i | j), anti-hermitian
+            return self._intor_raw("ipovlp")
+        if key == "int1e_cg_irxp":      # i (r - common origin) x p = (r - O) x nabla, anti-hermitian
+            return self._intor_raw("irxp", origin)
         if key == "int2e":
             return self.eri_full()
         raise KeyError(name)
@@ -313,3 +324,53 @@ def M(atom, basis="6-31G", charge=0, spin=0, unit="Angstrom", symmetry=False, ve
     """``gto.M`` equivalent."""
     return Mole(atom, basis=basis, charge=charge, spin=spin, unit=unit, symmetry=symmetry,
                 verbose=verbose)
+
+
+def chiral_mol(mol, tol: float = 1e-4) -> bool:
+    """``pyscf.gto.mole.chiral_mol(mol)``: True when the molecule cannot be
+    superimposed on its mirror image by a proper rotation (XTDA.py:818 gates the
+    rotatory strengths on it).
+
+    Mirror = reflection z -> -z about the charge centroid.  Candidate rotations
+    come from Kabsch fits of one non-collinear reference triple of the mirror
+    onto every charge- and distance-compatible triple of the original; the
+    molecule is achiral if one of them maps every atom onto an atom of equal
+    charge.  Linear and planar molecules are achiral outright.
+    """
+    x = np.asarray(mol.atom_coords(), dtype=np.float64)
+    z = np.asarray(mol.atom_charges())
+    n = len(z)
+    if n < 4:
+        return False
+    x = x - (z[:, None] * x).sum(0) / z.sum()
+    if np.linalg.svd(x, compute_uv=False)[-1] < tol * max(1.0, np.abs(x).max()):
+        return False                       # planar (or linear): the plane is a mirror
+    y = x * np.array([1.0, 1.0, -1.0])
+    dx = np.linalg.norm(x[:, None] - x[None], axis=-1)
+    # reference triple of the mirror: atoms 0, the farthest from it, then the one
+    # farthest from their line (non-collinear)
+    i0 = 0
+    i1 = int(np.argmax(dx[i0]))
+    u = (y[i1] - y[i0]) / np.linalg.norm(y[i1] - y[i0])
+    off = y - y[i0] - np.outer((y - y[i0]) @ u, u)
+    i2 = int(np.argmax(np.linalg.norm(off, axis=1)))
+    ref = [i0, i1, i2]
+    dref = dx[np.ix_(ref, ref)]          # mirror distances equal the original's
+
+    def kabsch(p, q):                      # proper rotation R with R p ~ q
+        h = p.T @ q
+        uu, _, vt = np.linalg.svd(h)
+        d = np.sign(np.linalg.det(vt.T @ uu.T))
+        return vt.T @ np.diag([1.0, 1.0, d]) @ uu.T
+
+    for a in np.where(z == z[i0])[0]:
+        for b in np.where((z == z[i1]) & (np.abs(dx[a] - dref[0, 1]) < 1e-3))[0]:
+            for c in np.where((z == z[i2]) & (np.abs(dx[a] - dref[0, 2]) < 1e-3)
+                              & (np.abs(dx[b] - dref[1, 2]) < 1e-3))[0]:
+                r = kabsch(y[ref], x[[a, b, c]])
+                yr = y @ r.T
+                d = np.linalg.norm(yr[:, None] - x[None], axis=-1)
+                d[z[:, None] != z[None, :]] = np.inf
+                if np.all(d.min(axis=1) < 1e-3):
+                    return False
+    return True

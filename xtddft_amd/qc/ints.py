@@ -214,6 +214,57 @@ class ShellPair:
                 out[i, j] = np.sum(self.cc * (tx + ty + tz))
         return out
 
+    # ket-side 1D tables (need kin=True: E extended to lb + 2):
+    #   D[i, j] = <i| d/dx |j> = j S[i, j-1] - 2 b S[i, j+1]
+    #   X[i, j] = <i| x - O |j> = S[i, j+1] + (B - O) S[i, j]
+    def _d1d(self, Sd):
+        b = np.broadcast_to(self.sb.exps[None, :], (self.sa.exps.size, self.sb.exps.size)).ravel()
+        la, lb = self.sa.l, self.sb.l
+        D = np.empty((la + 1, lb + 1, b.size))
+        for i in range(la + 1):
+            for j in range(lb + 1):
+                D[i, j] = -2.0 * b * Sd[i, j + 1] + (j * Sd[i, j - 1] if j >= 1 else 0.0)
+        return D
+
+    def deriv1(self):
+        """<a| d/dr_d |b> for d = x, y, z: (3, nca, ncb).  Needs kin=True."""
+        la, lb = self.sa.l, self.sb.l
+        S = [self._s1d(d) for d in range(3)]
+        D = [self._d1d(S[d]) for d in range(3)]
+        out = np.empty((3, len(cart_comps(la)), len(cart_comps(lb))))
+        for i, a in enumerate(cart_comps(la)):
+            for j, b in enumerate(cart_comps(lb)):
+                for d in range(3):
+                    f = D[d][a[d], b[d]]
+                    for e in range(3):
+                        if e != d:
+                            f = f * S[e][a[e], b[e]]
+                    out[d, i, j] = np.sum(self.cc * f)
+        return out
+
+    def angmom(self, origin):
+        """<a| ((r - origin) x nabla)_d |b>: (3, nca, ncb).  Needs kin=True."""
+        la, lb = self.sa.l, self.sb.l
+        S = [self._s1d(d) for d in range(3)]
+        D = [self._d1d(S[d]) for d in range(3)]
+        B = self.sb.center
+        X = []
+        for d in range(3):
+            Xd = np.empty((la + 1, lb + 1, self.p.size))
+            for i in range(la + 1):
+                for j in range(lb + 1):
+                    Xd[i, j] = S[d][i, j + 1] + (B[d] - origin[d]) * S[d][i, j]
+            X.append(Xd)
+        out = np.empty((3, len(cart_comps(la)), len(cart_comps(lb))))
+        for i, a in enumerate(cart_comps(la)):
+            for j, b in enumerate(cart_comps(lb)):
+                for d, (u, v) in enumerate(((1, 2), (2, 0), (0, 1))):
+                    w = 3 - u - v            # the untouched direction
+                    t1 = X[u][a[u], b[u]] * D[v][a[v], b[v]]     # (r-O)_u d_v
+                    t2 = X[v][a[v], b[v]] * D[u][a[u], b[u]]     # (r-O)_v d_u
+                    out[d, i, j] = np.sum(self.cc * (t1 - t2) * S[w][a[w], b[w]])
+        return out
+
     def multipole1(self, origin):
         """<a| (r - origin)_d |b> for d = x, y, z: (3, nca, ncb)."""
         la, lb = self.sa.l, self.sb.l

@@ -21,6 +21,8 @@ from .meanfield import MeanField
 from .operator import DeviceOperator
 from .utils import HA2EV, EVXNM, order_pyscf2my, so2st as _so2st
 
+CGS2AU = 1 / (235.7220 * 2)    # xtddft/utils/unit.py:9 (rotatory strength a.u. -> cgs)
+
 # PySCF TDBase defaults the reference copies (XTDA.py:29-31)
 CONV_TOL = 1e-5
 LINDEP = 1e-12
@@ -205,6 +207,48 @@ class XTDA:
         vt = self.v.T
         tdip = np.einsum('xi,yi->yx', da, vt[:, :na]) + np.einsum('xi,yi->yx', db, vt[:, na:])
         return 2. / 3. * np.einsum('s,sx,sx->s', self.e[:self.nstates], tdip, tdip)
+
+    def _qc_mol(self):
+        mol = self.mol if hasattr(self.mol, "intor") else self.mf.extra.get("qc_mol")
+        if mol is None or not hasattr(mol, "intor"):
+            raise ValueError("AO property integrals need a Mole with intor (xtddft_amd.qc)")
+        return mol
+
+    def rot_str(self, dip_ele_ao=None, dip_meg_ao=None):
+        """Rotatory strengths (XTDA.py:860-891): velocity-form electric
+        (``int1e_ipovlp``) and magnetic (``int1e_cg_irxp``, gauge origin 0)
+        transition dipoles, R = sum_x (1/w) mu_x m_x in cgs units (the
+        reference's ``unit.cgs2au``, Gaussian/ORCA convention)."""
+        if dip_ele_ao is None or dip_meg_ao is None:
+            mol = self._qc_mol()
+            dip_ele_ao = mol.intor('int1e_ipovlp', comp=3, hermi=2)
+            dip_meg_ao = mol.intor('int1e_cg_irxp', comp=3, hermi=2)
+        mf = self.mf
+        c = mf.mo_coeff
+        occ_a, vir_a = mf.mo_occ >= 1, mf.mo_occ == 0
+        occ_b, vir_b = mf.mo_occ >= 2, mf.mo_occ != 2
+        nv = self.nv
+        na = (self.nc + self.no) * nv
+        vt = self.v.T
+
+        def trans(op_ao):
+            a = np.einsum('xpq,pi,qj->xij', op_ao, c[:, occ_a], c[:, vir_a]).reshape(3, -1)
+            b = np.einsum('xpq,pi,qj->xij', op_ao, c[:, occ_b], c[:, vir_b]).reshape(3, -1)
+            b = b[:, self.order[na:] - na]
+            return np.einsum('xi,yi->yx', a, vt[:, :na]) + np.einsum('xi,yi->yx', b, vt[:, na:])
+        ele = -trans(dip_ele_ao)
+        meg = 0.5 * trans(dip_meg_ao)
+        omega = self.e[:self.nstates]
+        return np.einsum('s,sx,sx->s', 1.0 / omega, ele, meg) / CGS2AU
+
+    def properties(self):
+        """What XTDA.Davidson reports after the solve (XTDA.py:815-829): Delta<S^2>,
+        oscillator strengths and, for chiral molecules only, rotatory strengths."""
+        from .qc.gto import chiral_mol
+        mol = self._qc_mol()
+        self.os = self.osc_str()
+        self.rs = self.rot_str() if chiral_mol(mol) else np.zeros(self.nstates)
+        return self.dS2, self.os, self.rs
 
     def analyze(self, threshold=0.1, verbose=True):
         nc, nv, no = self.nc, self.nv, self.no
