@@ -1,32 +1,45 @@
 #!/usr/bin/env python
-"""Benchmark: X-TDA A.x throughput on MI355X (BASELINE.json metric).
+"""Benchmark: TDA A.x throughput on MI355X (BASELINE.json metric).
 
-    python bench.py --gpus N --steps K --warmup W
-    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config H|C1..C5|C4d]
 
-Workload (default): the BASELINE headline shape -- synthetic ROKS X-TDA,
+With ``--gpus N > 1`` outside a torch.distributed launch, this process starts
+``torch.distributed.run`` with N ranks (one process per GPU, RCCL over xGMI)
+before it touches the GPU and exits with the launcher's status; under
+torchrun (WORLD_SIZE set) it runs as one rank.
+
+Workload (default ``H``): the BASELINE headline shape -- synthetic ROKS X-TDA,
 nao = 1000, nocc_a/nocc_b = 101/99 (nc 99, no 2, nv 899), naux = 3 nao,
 ngrid = 1200 nao, GGA kernel + global hybrid (hyb 0.2), nvec = 20 trial
-vectors per A.x.  A "step" is one full A.x on the 20-vector batch (plus the
-RCCL all-reduce of sigma when N > 1).  value = matvecs/s = nvec*K / T where T
-is the max over ranks of the barrier+synchronise-bracketed wall time.
+vectors per A.x.  A "step" is one full A.x on the nvec-vector batch (plus the
+all-reduce of sigma when N > 1).  value = matvecs/s = nvec * K / T, T the max
+over ranks of the barrier + synchronise bracketed wall time of the K steps.
+The other BASELINE.json configs are parity-test shapes (tests/test_gpu_configs.py);
+``--config`` prints their lines for DESIGN.md.
 
-Multi-GPU: the DF aux index and the grid are sharded over ranks (each rank
-generates and holds only its shard); every rank computes a partial sigma for
-all vectors and one all-reduce (torch.distributed / RCCL over xGMI) sums them:
-fixed total work, so "scaling": "strong".
+Multi-GPU: the grid is sharded over ranks and the DF factor replicated with an
+aux window + a row block of the stored exchange per rank (``DeviceOperator``
+partition); each rank computes a partial sigma of all vectors, one all-reduce
+sums them: fixed total work, "scaling": "strong".
 
-Extra JSON fields: roofline (dominant GEMM class timed live with HIP events
-on the library's stream over the timed steps), cpu_baseline (the NumPy
-oracle = the reference's AO-route algorithm, timed on this host on a bounded
-sample and extrapolated), converge (wall time of the device Davidson to
-nroots = 20 on the same operator, N = 1 only).
+Extra JSON fields: roofline (dominant GEMM class timed live with HIP events on
+the library's stream over the timed steps; traffic from this config's committed
+rocprofv3 PMC summary), cpu_baseline (the NumPy oracle = the reference's AO
+route, timed on this host's cores), converge (wall time of the device Davidson
+to nroots with the reference's criteria, including operator construction).
+
+``XT_BENCH_OPERATOR=module:function`` replaces the operator factory (the CPU
+launcher test uses a stub from tests/); ``XT_BENCH_BACKEND=gloo`` rehearses the
+N-rank path with ranks sharing the visible GPU(s).
 """
 from __future__ import annotations
 
 import argparse
+import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -37,109 +50,170 @@ sys.path.insert(0, ROOT)
 
 FP64_PEAK_TFLOPS = 78.6     # MI355X dense FP64 matrix peak (AMD spec); 74.2 measured (tools/mfma_probe.hip)
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8.0 TB/s spec
-
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_summary.json")
 
 KIND_NAME = {"XTDA": "X-TDA", "SF_UP": "SF-TDA (spin-flip up)", "SF_DOWN": "SF-TDA (spin-flip down)",
              "XSF": "XSF-TDA"}
 
+# BASELINE.json configs as synthetic shapes (SURVEY.md 8 shape table): nao, closed /
+# open shells, operator, vectors per A.x (= nroots), hybrid fraction, J/K model.
+# C4 (C60- doublet) is ill-posed for spin adaptation (XSF divides by 2S - 1 = 0,
+# XSF_TDA.py:1102-1121): C4 is the quartet shape (no = 3, SA = 3, OO compressed),
+# C4d the doublet at SA = 0.  C5 is the exact-K path: stored 8-fold ERIs.
+CONFIGS = {
+    "H": dict(nao=1000, nc=99, no=2, kind="XTDA", nvec=20, nroots=20, hyb=0.2),
+    "C1": dict(nao=13, nc=3, no=2, kind="XTDA", nvec=5, nroots=5, hyb=0.2, ngrid=35000),
+    "C2": dict(nao=180, nc=33, no=1, kind="XTDA", nvec=20, nroots=20, hyb=0.2),
+    "C3": dict(nao=861, nc=91, no=4, kind="SF_UP", nvec=30, nroots=30, hyb=0.5),
+    "C4": dict(nao=840, nc=179, no=3, kind="XSF", nvec=40, nroots=40, hyb=0.5, sa=3, remove=True),
+    "C4d": dict(nao=840, nc=180, no=1, kind="XSF", nvec=40, nroots=40, hyb=0.5, sa=0, remove=True),
+    "C5": dict(nao=152, nc=35, no=2, kind="XTDA", nvec=50, nroots=50, hyb=0.2, jk="ERI8"),
+}
+CONFIG_NAMES = {"H": "headline", "C1": "CH2 triplet / 6-31G", "C2": "naphthalene+ / def2-SVP",
+                "C3": "Fe(II)P quintet / def2-TZVP", "C4": "C60-like quartet / def2-SVP",
+                "C4d": "C60- doublet / def2-SVP", "C5": "[Cu2O2]2+ triplet / def2-TZVP"}
 
-def parse():
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--nao", type=int, default=1000)
-    ap.add_argument("--nc", type=int, default=99)
-    ap.add_argument("--no", type=int, default=2)
+    ap.add_argument("--config", default="H", choices=sorted(CONFIGS),
+                    help="BASELINE.json shape preset (synthetic data of that shape)")
+    ap.add_argument("--nao", type=int, default=None)
+    # (long names: torch.distributed.run re-parses the script's argv and rejects
+    # abbreviations of its own options such as --no / --node-rank)
+    ap.add_argument("--nclosed", dest="nc", type=int, default=None)
+    ap.add_argument("--nopen", dest="no", type=int, default=None)
     ap.add_argument("--naux", type=int, default=None)
     ap.add_argument("--ngrid", type=int, default=None)
-    ap.add_argument("--nvec", type=int, default=20)
+    ap.add_argument("--nvec", type=int, default=None)
+    ap.add_argument("--nroots", type=int, default=None)
     ap.add_argument("--xc", default="GGA")
-    ap.add_argument("--hyb", type=float, default=0.2)
+    ap.add_argument("--hyb", type=float, default=None)
+    ap.add_argument("--kind", default=None, choices=["XTDA", "SF_UP", "SF_DOWN", "XSF"])
+    ap.add_argument("--sa", type=int, default=None, help="XSF spin-adaptation level (XSF_TDA.py SA)")
+    ap.add_argument("--jk", default=None, choices=["DF", "ERI8"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-converge", action="store_true")
     ap.add_argument("--converge", action="store_true", help="also at N > 1")
-    ap.add_argument("--nroots", type=int, default=20)
     ap.add_argument("--k-mode", default="auto", choices=["auto", "direct", "stored"],
                     help="exchange evaluation (xt_set_exchange_mode)")
-    ap.add_argument("--kind", default="XTDA", choices=["XTDA", "SF_UP", "SF_DOWN", "XSF"],
-                    help="operator (XTDA.py / SF_TDA.py / XSF_TDA.py vind)")
-    ap.add_argument("--sa", type=int, default=0, help="XSF spin-adaptation level (XSF_TDA.py SA)")
-    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
-                    help="BASELINE.json shape preset (synthetic data of that shape); the default "
-                         "bench line is the headline H")
-    args = ap.parse_args()
-    if args.config:
-        for k, v in CONFIGS[args.config].items():
+    args = ap.parse_args(argv)
+    preset = dict(sa=0, remove=False, jk="DF", ngrid=None)
+    preset.update(CONFIGS[args.config])
+    for k, v in preset.items():
+        if getattr(args, k, None) is None:
             setattr(args, k, v)
+    args.nv = args.nao - args.nc - args.no
+    args.naux = args.naux or 3 * args.nao
+    args.ngrid = args.ngrid or 1200 * args.nao
     return args
 
 
-# BASELINE.json configs as synthetic shapes (SURVEY.md 8 shape table): nao, closed /
-# open shells, operator, vectors per A.x (= nroots), hybrid fraction.  C4 is the
-# XSF doublet, run at SA = 0 (SA > 0 divides by 2S - 1 = 0, XSF_TDA.py:1102-1121).
-CONFIGS = {
-    "H": dict(nao=1000, nc=99, no=2, kind="XTDA", nvec=20, nroots=20, hyb=0.2),
-    "C2": dict(nao=180, nc=33, no=1, kind="XTDA", nvec=20, nroots=20, hyb=0.2),
-    "C3": dict(nao=861, nc=91, no=4, kind="SF_UP", nvec=30, nroots=30, hyb=0.5),
-    "C4": dict(nao=840, nc=180, no=1, kind="XSF", nvec=40, nroots=40, hyb=0.5, sa=0),
-    "C5": dict(nao=152, nc=35, no=2, kind="XTDA", nvec=50, nroots=50, hyb=0.2),
-}
+# ---------------------------------------------------------------------------
+# launcher: N ranks under torch.distributed.run, started before any GPU use
+# ---------------------------------------------------------------------------
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
-def cpu_baseline(args):
-    """Oracle (reference AO-route algorithm, NumPy/BLAS) on this host.
-
-    t(naux, ngrid) per trial vector is linear in both sizes; it is timed at
-    three bounded samples of the SAME shape (nao, nc, no) and extrapolated to
-    the full naux / ngrid.  Returns matvecs/s.
-    """
-    from oracle import xtda as oxtda
-    from xtddft_amd.synthetic import make_mf, make_trial_vectors
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:
-        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    naux = args.naux or 3 * args.nao
-    ngrid = args.ngrid or 1200 * args.nao
-    samples = [(16, 8192), (32, 8192), (16, 16384)]
-    times = []
-    t_all = time.perf_counter()
-    for n, g in samples:
-        mf = make_mf(nao=args.nao, nc=args.nc, no=args.no, naux=n, ngrid=g, xctype=args.xc,
-                     hyb=args.hyb)
-        vind, hdiag = oxtda.gen_tda_operation(mf)
-        z = make_trial_vectors(1, hdiag.size)
-        vind(z)                        # warm-up (SURVEY.md 8(d): 1 warm-up, median of >= 5)
-        ts = []
-        for _ in range(5):
-            t0 = time.perf_counter(); vind(z); ts.append(time.perf_counter() - t0)
-        times.append(float(np.median(ts)))
-        del mf, vind
-    (n1, g1), (n2, _), (_, g3) = samples
-    a = (times[1] - times[0]) / (n2 - n1)
-    b = (times[2] - times[0]) / (g3 - g1)
-    t0 = times[0] - a * n1 - b * g1
-    t_vec = t0 + a * naux + b * ngrid
-    return dict(value=1.0 / t_vec, unit="matvecs/s", cores=int(cores), kind="port",
-                sample=(f"oracle X-TDA vind (NumPy AO route, DF J/K, GGA) on 1 vector at nao={args.nao}, "
-                        f"(naux, ngrid) in {samples}, 1 warm-up + median of 5; linear extrapolation to "
-                        f"naux={naux}, ngrid={ngrid}: t_vec = {t_vec:.1f} s"),
-                host=_host_info(), sample_wall_s=round(time.perf_counter() - t_all, 1))
+def launch(args, argv):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
+# ---------------------------------------------------------------------------
+# the operator under test
+# ---------------------------------------------------------------------------
+class Workload:
+    """What a factory returns: the operator, its mean field, the torch device the
+    trial vectors live on, and the setup split (synthetic generation vs operator
+    construction = MO transforms + xt_prepare)."""
+
+    def __init__(self, op, mf, device, t_gen, t_op, replicate):
+        self.op, self.mf, self.device = op, mf, device
+        self.t_gen, self.t_op, self.replicate = t_gen, t_op, replicate
+
+
+def _eri8_from_device_factor(cderi):
+    """8-fold packed ERIs (mu nu|la si) = sum_P B B from a device DF factor
+    (synthetic exact-K input; PySCF 's8' order, ij = i(i+1)/2 + j)."""
+    import torch
+    nao = cderi.shape[1]
+    ii, jj = torch.tril_indices(nao, nao, device=cderi.device)
+    b2 = cderi[:, ii, jj]                       # (naux, npair)
+    e = b2.T @ b2                               # (npair, npair)
+    pi, pj = torch.tril_indices(e.shape[0], e.shape[0], device=cderi.device)
+    return e[pi, pj].contiguous()
+
+
+def device_workload(args, rank, world, local):
+    import torch
+    from xtddft_amd.operator import DeviceOperator
+    from xtddft_amd.synthetic import make_device_mf
+    from xtddft_amd.xsf_tda import get_vect
+    replicate = world > 1 and args.k_mode != "direct"
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    mf = make_device_mf(nao=args.nao, nc=args.nc, no=args.no, naux=args.naux, ngrid=args.ngrid,
+                        xctype=args.xc, hyb=args.hyb, device=local, shard=(rank, world),
+                        full_aux=replicate or args.jk == "ERI8")
+    if args.jk == "ERI8":
+        mf.eri = _eri8_from_device_factor(mf.cderi)
+        mf.cderi = None
+        mf.chol_tol = 0.0
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t0
+    kw = {}
+    if args.kind == "XSF":
+        # XSF_TDA.kernel default fglobal = (1 - d_lda) c_x + d_lda, d_lda = 0.3, c_x = hyb
+        kw = dict(sa=args.sa, fglobal=0.7 * args.hyb + 0.3, foo=1.0, remove=bool(args.remove))
+    t1 = time.perf_counter()
+    op = DeviceOperator(mf, args.kind, shard=(rank, world), device=local, **kw,
+                        presharded="grid" if (replicate or args.jk == "ERI8") else True,
+                        k_mode=args.k_mode, replicate_df=replicate)
+    if args.kind == "XSF" and args.remove:
+        op.set_oo_basis(get_vect(args.no))
+    torch.cuda.synchronize()
+    t_op = time.perf_counter() - t1
+    mf.cderi = None
+    mf.eri = None
+    mf.grids = None
+    mf.fxc = None
+    mf.fxc_sf = None
+    torch.cuda.empty_cache()
+    return Workload(op, mf, torch.device(f"cuda:{local}"), t_gen, t_op, replicate)
+
+
+def _factory():
+    spec = os.environ.get("XT_BENCH_OPERATOR")
+    if not spec:
+        return device_workload
+    mod, fn = spec.split(":")
+    return getattr(importlib.import_module(mod), fn)
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (BASELINE.md 3): the oracle on this host's cores
+# ---------------------------------------------------------------------------
 def _host_info():
     """CPU model and BLAS build of the host timing the CPU baseline."""
-    info = {}
+    info = {"host_cpus": os.cpu_count()}
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
                     info["cpu"] = line.split(":", 1)[1].strip()
                     break
-        info["host_cpus"] = os.cpu_count()
-    except Exception:
+    except OSError:
         pass
     try:
         from threadpoolctl import threadpool_info
@@ -150,81 +224,214 @@ def _host_info():
     return info
 
 
-def load_traffic(tag_name):
-    """HBM bytes per launch of the tagged kernel from a committed rocprofv3 PMC summary."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+def _oracle_vind(args, mf):
+    from oracle import sf_tda as osf
+    from oracle import xsf_tda as oxsf
+    from oracle import xtda as oxtda
+    if args.kind == "XTDA":
+        return oxtda.gen_tda_operation(mf)
+    if args.kind in ("SF_UP", "SF_DOWN"):
+        return osf.gen_tda_operation_sf(mf, 1 if args.kind == "SF_UP" else -1)
+    o = oxsf.XSFOracle(mf, SA=args.sa)
+    o.re = bool(args.remove)
+    return o.gen_tda_operation_sf(fglobal=0.7 * args.hyb + 0.3)
+
+
+def _time_call(f, reps):
+    f()                                  # 1 warm-up
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        f()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts))
+
+
+def cpu_baseline(args):
+    """The oracle's A.x (the reference's AO-route algorithm, NumPy/BLAS) on ALL
+    host cores, one trial vector per call, 1 warm-up + median of 5.
+
+    Small shapes are timed at the full (naux, ngrid).  Large ones at the full
+    naux and two bounded grid sizes: the grid loop is blockwise, so t(ngrid)
+    is linear and only the grid dimension is extrapolated.  Returns matvecs/s."""
+    from threadpoolctl import threadpool_info, threadpool_limits
+    from xtddft_amd.synthetic import as_eri8, make_mf, make_trial_vectors
+    ncpu = os.cpu_count() or 1
+    t_all = time.perf_counter()
+    with threadpool_limits(limits=ncpu):
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()
+                       if i.get("user_api") == "blas"] or [1])
+        mkind = "RO"
+
+        def t_vec(ngrid):
+            mf = make_mf(nao=args.nao, nc=args.nc, no=args.no, naux=args.naux, ngrid=ngrid,
+                         xctype=args.xc, hyb=args.hyb, kind=mkind)
+            if args.jk == "ERI8":
+                mf = as_eri8(mf)
+            vind, hdiag = _oracle_vind(args, mf)
+            z = make_trial_vectors(1, hdiag.size)
+            return _time_call(lambda: vind(z), 5)
+        # full size when the AO-route grid data stay small (< 4 GB)
+        full = 8.0 * 4 * args.ngrid * args.nao < 4e9
+        if full:
+            t = t_vec(args.ngrid)
+            how = f"measured at the full size (naux={args.naux}, ngrid={args.ngrid})"
+        else:
+            g1, g2 = 8192, 24576
+            ta, tb = t_vec(g1), t_vec(g2)
+            slope = (tb - ta) / (g2 - g1)
+            t = ta + slope * (args.ngrid - g1)
+            how = (f"measured at the full naux={args.naux} with ngrid {g1} ({ta:.2f} s) and {g2} "
+                   f"({tb:.2f} s); linear in ngrid to {args.ngrid}")
+    return dict(value=1.0 / t, unit="matvecs/s", cores=int(threads), kind="port",
+                sample=(f"oracle {KIND_NAME[args.kind]} vind (NumPy AO route, {args.jk} J/K, {args.xc}) "
+                        f"on 1 vector at nao={args.nao}, {how}; 1 warm-up + median of 5; "
+                        f"t_vec = {t:.2f} s"),
+                host=_host_info(), sample_wall_s=round(time.perf_counter() - t_all, 1))
+
+
+# ---------------------------------------------------------------------------
+# Davidson to nroots on the same operator (reference criteria per kind)
+# ---------------------------------------------------------------------------
+def converge(args, w, allreduce):
+    import torch
+    from xtddft_amd.davidson import DiagPrecond, davidson1
+    mf, op, dev = w.mf, w.op, w.device
+    if args.kind == "XTDA":
+        from xtddft_amd.xtda import XTDA
+        x = XTDA.__new__(XTDA)
+        x.mf, x.X, x.nstates, x.device = mf, True, args.nroots, dev.index
+        hdiag = x._hdiag()
+        x0 = x.get_init_guess(mf, args.nroots)
+
+        def pickeig(wv, v, nroots, envs):
+            idx = np.where(wv > 0.001)[0]
+            return wv[idx], v[:, idx], idx
+        kw = dict(tol_residual=1e-5, lindep=1e-12, pick=pickeig, max_cycle=100)
+        pre = DiagPrecond(hdiag, 0.0, dev.index)
+        crit = "|de|<1e-12, |r|<1e-5, pick w>1e-3 (XTDA.py:769-777)"
+    elif args.kind in ("SF_UP", "SF_DOWN"):
+        from xtddft_amd.sf_tda import init_guess, sf_hdiag
+        isf = 1 if args.kind == "SF_UP" else -1
+        hdiag = sf_hdiag(mf, isf)
+        x0 = init_guess(mf, args.nroots, isf)
+        kw = dict(tol=1e-7, lindep=1e-14, max_cycle=3000)
+        pre = DiagPrecond(hdiag, 1e-3, dev.index)
+        crit = "tol 1e-7, lindep 1e-14 (SF_TDA.py:392-395)"
+    else:
+        from xtddft_amd.xsf_tda import XSF_TDA, get_vect
+        x = XSF_TDA(mf, SA=args.sa, device=dev.index)
+        x.re = bool(args.remove)
+        x.vects = get_vect(args.no)
+        x.nstates = args.nroots
+        fg = 0.7 * args.hyb + 0.3
+        hdiag = x._build_preconditioner_hdiag(fg, op)
+        if x.re:
+            hdiag = x._compress_removed_hdiag(hdiag)
+        x0 = x.init_guess(args.nroots, hdiag)
+        kw = dict(tol=1e-8, lindep=1e-9, max_cycle=1000)
+        pre = DiagPrecond(hdiag, 1e-3, dev.index)
+        crit = "tol 1e-8, lindep 1e-9 (XSF_TDA.py:1467-1470)"
+    stats = dict(calls=0, vectors=0, s=0.0)
+
+    def aop(xt):
+        t = time.perf_counter()
+        s = op.apply(xt)
+        allreduce(s)
+        torch.cuda.synchronize()
+        stats["calls"] += 1
+        stats["vectors"] += int(s.shape[0])
+        stats["s"] += time.perf_counter() - t
+        return s
+    torch.cuda.synchronize()
+    tc = time.perf_counter()
+    conv, e, _, icyc = davidson1(aop, x0, pre, nroots=args.nroots, device=dev.index,
+                                 return_device=True, **kw)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - tc
+    return dict(nroots=args.nroots, wall_s=round(wall + w.t_op, 2), davidson_s=round(wall, 2),
+                operator_setup_s=round(w.t_op, 2), iterations=int(icyc) + 1,
+                converged=bool(np.all(conv)), ax_calls=stats["calls"], ax_vectors=stats["vectors"],
+                ax_s=round(stats["s"], 2), e_min_ha=float(e[0]), criteria=crit)
+
+
+# ---------------------------------------------------------------------------
+def load_traffic(config, tag_name):
+    """HBM bytes per launch of the tagged kernel from this config's committed
+    rocprofv3 PMC summary (profiles/r02_pmc_summary.json), None if absent."""
     try:
-        with open(path) as f:
+        with open(PMC_SUMMARY) as f:
             d = json.load(f)
-        return d.get(tag_name, {}).get("hbm_bytes_per_launch")
-    except Exception:
+        return d.get(config, {}).get(tag_name, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
         return None
 
 
-def main():
-    args = parse()
+def roofline_of(args, stats_acc, steps):
+    dom_name, dom = max(stats_acc.items(), key=lambda kv: kv[1]["ms"])
+    avg_ms = dom["ms"] / max(1, dom["launches"])
+    traffic = load_traffic(args.config, dom_name)
+    if dom_name == "mo_exchange_stored":
+        # HBM-bound: streams the stored exchange matrix once per launch (+ Ze in, sigma in/out)
+        occ = args.nc if args.kind == "SF_UP" else args.nc + args.no
+        vir = args.nv if args.kind == "SF_UP" else args.no + args.nv
+        ov = occ * vir
+        nzg = (2 if args.kind == "XTDA" else 1) * args.nvec
+        bytes_launch = 8.0 * (ov * ov + 3.0 * nzg * ov)
+        gbs = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        return dict(bound="hbm", achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(gbs / HBM_PEAK_GBS, 4), traffic=traffic, kernel=dom_name,
+                    avg_launch_ms=round(avg_ms, 4), bytes_per_launch=bytes_launch,
+                    launches_per_step=dom["launches"] / steps)
+    flops_launch = dom["flops"] / max(1, dom["launches"])
+    achieved = flops_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+    return dict(bound="mfma", achieved=round(achieved, 3), peak=FP64_PEAK_TFLOPS, unit="TFLOP/s",
+                frac=round(achieved / FP64_PEAK_TFLOPS, 4), traffic=traffic,
+                kernel=dom_name, avg_launch_ms=round(avg_ms, 4),
+                flops_per_launch=flops_launch, launches_per_step=dom["launches"] / steps)
+
+
+def rank_main(args):
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("for --gpus N > 1 launch with torch.distributed.run (one process per GPU)")
-    # XT_BENCH_BACKEND=gloo rehearses the N-rank path with ranks sharing the visible
-    # GPU(s) (tests on a one-GPU box); the real runs use nccl = RCCL over xGMI
     backend = os.environ.get("XT_BENCH_BACKEND", "nccl")
-    if backend != "nccl":
-        local = local % torch.cuda.device_count()
-    torch.cuda.set_device(local)
+    stub = bool(os.environ.get("XT_BENCH_OPERATOR"))
+    use_gpu = not stub
+    if use_gpu:
+        if backend != "nccl":     # gloo rehearsal: ranks share the visible GPU(s)
+            local = local % torch.cuda.device_count()
+        torch.cuda.set_device(local)
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
             dist.init_process_group(backend)
-    from xtddft_amd import build
-    if rank == 0:
-        build.build()
-    if world > 1:
-        dist.barrier()
-    from xtddft_amd.synthetic import make_device_mf
-    from xtddft_amd.operator import DeviceOperator
+    if use_gpu:
+        from xtddft_amd import build
+        if rank == 0:
+            build.build()
+        if world > 1:
+            dist.barrier()
+    from xtddft_amd.parallel import allreduce_sigma
 
-    naux = args.naux or 3 * args.nao
-    ngrid = args.ngrid or 1200 * args.nao
-    nv = args.nao - args.nc - args.no
-    t_setup = time.perf_counter()
-    # stored exchange over N ranks: the MO factor is replicated and each rank
-    # keeps 1/N of the exchange rows (xt_set_partition); direct: aux-sliced factor
-    replicate = world > 1 and args.k_mode != "direct"
-    mf = make_device_mf(nao=args.nao, nc=args.nc, no=args.no, naux=naux, ngrid=ngrid,
-                        xctype=args.xc, hyb=args.hyb, device=local, shard=(rank, world),
-                        full_aux=replicate)
-    kw = {}
-    if args.kind == "XSF":
-        # XSF_TDA.kernel default fglobal = (1 - d_lda) c_x + d_lda, d_lda = 0.3, c_x = hyb
-        kw = dict(sa=args.sa, fglobal=0.7 * args.hyb + 0.3, foo=1.0, remove=False)
-    op = DeviceOperator(mf, args.kind, shard=(rank, world), device=local, **kw,
-                        presharded="grid" if replicate else True, k_mode=args.k_mode,
-                        replicate_df=replicate)
-    mf.cderi = None
-    mf.grids = None
-    mf.fxc = None
-    mf.fxc_sf = None
-    torch.cuda.synchronize()
-    torch.cuda.empty_cache()
-    t_setup = time.perf_counter() - t_setup
+    def sync():
+        if use_gpu:
+            torch.cuda.synchronize()
 
-    gen = torch.Generator(device=f"cuda:{local}")
+    w = _factory()(args, rank, world, local)
+    op = w.op
+    gen = torch.Generator(device=w.device)
     gen.manual_seed(20261016)
-    z = torch.randn((args.nvec, op.dim), dtype=torch.float64, device=f"cuda:{local}", generator=gen)
+    z = torch.randn((args.nvec, op.dim), dtype=torch.float64, device=w.device, generator=gen)
     z /= z.norm(dim=1, keepdim=True)
     out = torch.empty_like(z)
 
     def step():
         op.apply(z, out)
-        if world > 1:
-            dist.all_reduce(out)
+        allreduce_sigma(out)
 
     for _ in range(args.warmup):
         step()
@@ -232,51 +439,33 @@ def main():
     stats_acc = {}
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         for name, s in op.profile_stats().items():
             a = stats_acc.setdefault(name, dict(ms=0.0, launches=0, flops=0.0))
             a["ms"] += s["ms"]; a["launches"] += s["launches"]; a["flops"] += s["flops"]
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     op.set_profile(0)
-    tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+    tt = torch.tensor([dt], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     T = float(tt.item())
+    verify = w.verify(z, out) if hasattr(w, "verify") else None   # a workload's own self-check
     phases = op.last_timings()
-
-    # dominant GEMM class on this rank
-    dom_name, dom = max(stats_acc.items(), key=lambda kv: kv[1]["ms"])
-    avg_ms = dom["ms"] / max(1, dom["launches"])
-    flops_launch = dom["flops"] / max(1, dom["launches"])
-    achieved = flops_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
-    traffic = load_traffic(dom_name)
-    if dom_name == "mo_exchange_stored":
-        # HBM-bound: streams the stored exchange matrix once per launch (+ Ze in, sigma in/out)
-        occ = args.nc if args.kind == "SF_UP" else args.nc + args.no
-        vir = nv if args.kind == "SF_UP" else args.no + nv
-        ov = occ * vir
-        nzg = (2 if args.kind == "XTDA" else 1) * args.nvec
-        bytes_launch = 8.0 * (ov * ov + 3.0 * nzg * ov)
-        gbs = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        roofline = dict(bound="hbm", achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(gbs / HBM_PEAK_GBS, 4), traffic=traffic, kernel=dom_name,
-                        avg_launch_ms=round(avg_ms, 4), bytes_per_launch=bytes_launch,
-                        launches_per_step=dom["launches"] / args.steps)
-    else:
-        roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=FP64_PEAK_TFLOPS, unit="TFLOP/s",
-                        frac=round(achieved / FP64_PEAK_TFLOPS, 4), traffic=traffic,
-                        kernel=dom_name, avg_launch_ms=round(avg_ms, 4),
-                        flops_per_launch=flops_launch, launches_per_step=dom["launches"] / args.steps)
+    roofline = roofline_of(args, stats_acc, args.steps)
     others = {k: dict(ms_per_step=round(v["ms"] / args.steps, 3),
                       tflops=round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 3))
-              for k, v in stats_acc.items()}
-
+              for k, v in stats_acc.items() if v["launches"]}
+    workload = (f"{KIND_NAME[args.kind]} A.x, nao={args.nao}, nocc_a/nocc_b={args.nc + args.no}/{args.nc}, "
+                f"dim={op.dim}, nvec={args.nvec}, {args.jk} naux={args.naux}, ngrid={args.ngrid}, "
+                f"xc={args.xc}, hyb={args.hyb}"
+                + (f", SA={args.sa}, remove={bool(args.remove)}" if args.kind == "XSF" else "")
+                + f" [BASELINE {args.config}: {CONFIG_NAMES[args.config]}]")
     result = dict(
         metric="A·x matvecs/sec (nao, nocc×nvir, nvec)",
         value=round(args.nvec * args.steps / T, 4),
@@ -284,71 +473,42 @@ def main():
         n_gpus=world, steps=args.steps, warmup=args.warmup,
         ms_per_step=round(1e3 * T / args.steps, 3),
         higher_is_better=True, scaling="strong", vs_baseline=None, dtype="f64",
-        data="synthetic (seeded ROKS mean field, DF factor, GGA grid kernel; generated in HBM)",
-        config=dict(workload=(f"{KIND_NAME[args.kind]} A.x, nao={args.nao}, nocc_a/nocc_b={args.nc + args.no}/{args.nc}, "
-                              f"dim={op.dim}, "
-                              f"nvec={args.nvec}, naux={naux}, ngrid={ngrid}, xc={args.xc}, hyb={args.hyb}"
-                              + (f", SA={args.sa}" if args.kind == "XSF" else "")
-                              + (f" [BASELINE {args.config}]" if args.config else "")),
-                    nao=args.nao, dim=op.dim, nvec=args.nvec, naux=naux, ngrid=ngrid,
-                    parallelism=(f"grid sharded x{world}; " +
-                                 ("replicated MO DF factor, aux window + stored-exchange rows"
-                                  if replicate else "aux sharded") +
-                                 " per rank; RCCL all-reduce of sigma")),
+        data=("synthetic (seeded ROKS mean field, DF factor, GGA grid kernel; generated in HBM)"
+              if not stub else "STUB operator (launcher test only; not a measurement)"),
+        config=dict(workload=workload, nao=args.nao, dim=op.dim, nvec=args.nvec, naux=args.naux,
+                    ngrid=args.ngrid, parallelism=(
+                        f"grid sharded x{world}; " +
+                        ("replicated MO DF factor, aux window + stored-exchange rows"
+                         if w.replicate else "aux sharded") + " per rank; all-reduce of sigma")),
         roofline=roofline,
         gemm_classes=others,
         phases_ms_last_step=phases,
-        setup_s=round(t_setup, 2),
+        setup_s=dict(synthetic_generation=round(w.t_gen, 2), operator_construction=round(w.t_op, 2)),
         exchange=dict(mode=op.k_mode, stored_gib=round(op.k_gib, 2), build_s=round(op.prepare_s, 3)),
     )
-
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.kind == "XTDA":
+    if verify is not None:
+        result["verify"] = verify
+    if rank == 0 and world == 1 and use_gpu and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(args)
         except Exception as e:   # report, never hide
             result["cpu_baseline"] = dict(value=None, error=repr(e))
-
-    if ((world == 1 and not args.no_converge) or args.converge) and args.kind == "XTDA":
-        from xtddft_amd.davidson import DiagPrecond, davidson1
-        from xtddft_amd.xtda import XTDA
-        x = XTDA.__new__(XTDA)
-        x.mf, x.X, x.nstates, x.device = mf, True, args.nroots, local
-        hdiag = x._hdiag()
-        x0 = x.get_init_guess(mf, args.nroots)
-
-        aop_stats = dict(calls=0, vectors=0, s=0.0)
-
-        def aop(xt):
-            t = time.perf_counter()
-            s = op.apply(xt)
-            if world > 1:
-                dist.all_reduce(s)
-            torch.cuda.synchronize()
-            aop_stats["calls"] += 1
-            aop_stats["vectors"] += int(s.shape[0])
-            aop_stats["s"] += time.perf_counter() - t
-            return s
-
-        def pickeig(w, v, nroots, envs):
-            idx = np.where(w > 0.001)[0]
-            return w[idx], v[:, idx], idx
-        torch.cuda.synchronize()
-        tc = time.perf_counter()
-        conv, e, _, icyc = davidson1(aop, x0, DiagPrecond(hdiag, 0.0, local), tol_residual=1e-5,
-                                     lindep=1e-12, nroots=args.nroots, pick=pickeig, max_cycle=100,
-                                     device=local, return_device=True)
-        torch.cuda.synchronize()
-        wall = time.perf_counter() - tc
-        result["converge"] = dict(nroots=args.nroots, wall_s=round(wall, 2),
-                                  wall_s_incl_exchange_build=round(wall + op.prepare_s, 2),
-                                  iterations=int(icyc) + 1, converged=bool(np.all(conv)),
-                                  ax_vectors=aop_stats["vectors"], ax_s=round(aop_stats["s"], 2),
-                                  e_min_ha=float(e[0]), criteria="|de|<1e-12, |r|<1e-5 (XTDA.py:775)")
+    if use_gpu and ((world == 1 and not args.no_converge) or args.converge):
+        result["converge"] = converge(args, w, allreduce_sigma)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch(args, argv)
+    return rank_main(args)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -60,6 +60,10 @@ int xt_destroy(xt_ctx* ctx);
 int xt_set_stream(xt_ctx* ctx, void* hip_stream);
 const char* xt_last_error(void);
 int xt_abi_version(void);
+/* SHA-256 prefix of the sources, headers and flags the library was built from
+   (xtddft_amd/build.py source_hash); the Python loader refuses a library whose
+   id differs from its tree. */
+const char* xt_build_id(void);
 
 /* one-time setup (what the reference builds once per solve) ------------ */
 /* MO coefficients (nao x nmo); c_beta ignored when restricted.

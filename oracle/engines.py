@@ -46,10 +46,15 @@ def get_jk(cderi, dms, with_j=True, with_k=True):
         gam = np.einsum('pmn,xmn->xp', cderi, d, optimize=True)
         vj = np.einsum('xp,pmn->xmn', gam, cderi, optimize=True).reshape(shape)
     if with_k:
-        vk = np.empty_like(d)
+        # chunked over P so the (P, nao, nao) intermediate stays bounded at large naux
+        naux, nao = cderi.shape[0], shape[-1]
+        pc = max(1, min(naux, (1 << 29) // (8 * nao * nao)))
+        vk = np.zeros_like(d)
         for x in range(d.shape[0]):
-            t = np.matmul(cderi, d[x])               # (naux, nao, nao): B_P D
-            vk[x] = np.einsum('pml,pln->mn', t, cderi, optimize=True)
+            for p0 in range(0, naux, pc):
+                b = cderi[p0:p0 + pc]
+                t = np.matmul(b, d[x])               # (pc, nao, nao): B_P D
+                vk[x] += np.einsum('pml,pln->mn', t, b, optimize=True)
         vk = vk.reshape(shape)
     return vj, vk
 

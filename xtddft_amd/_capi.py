@@ -27,7 +27,8 @@ EXPORTS = [
     "xt_set_orbitals", "xt_set_fock_mo", "xt_set_orbital_energies", "xt_set_jk_df",
     "xt_set_jk_eri8", "xt_naux",
     "xt_set_grid", "xt_set_oo_basis", "xt_apply", "xt_dim", "xt_last_timings",
-    "xt_xsf_j_diagonals", "xt_set_exchange_mode", "xt_prepare", "xt_set_partition", "xt_set_profile", "xt_profile_stats", "xt_dgemm", "xt_precond", "xt_row_norms2", "xt_row_scale",
+    "xt_xsf_j_diagonals", "xt_set_exchange_mode", "xt_prepare", "xt_set_partition", "xt_set_profile",
+    "xt_profile_stats", "xt_dgemm", "xt_precond", "xt_row_norms2", "xt_row_scale", "xt_build_id",
 ]
 
 
@@ -75,6 +76,7 @@ def lib():
     L.xt_destroy.argtypes = [vp]
     L.xt_set_stream.argtypes = [vp, vp]
     L.xt_last_error.restype = ctypes.c_char_p
+    L.xt_build_id.restype = ctypes.c_char_p
     L.xt_set_orbitals.argtypes = [vp, dp, dp, c_int]
     L.xt_set_fock_mo.argtypes = [vp, dp, dp, dp, dp, c_int]
     L.xt_set_orbital_energies.argtypes = [vp, dp, dp, c_int]
@@ -102,6 +104,12 @@ def lib():
             raise LibraryMissing(f"{LIB_PATH} lacks symbol {name}")
     if L.xt_abi_version() != ABI_VERSION:
         raise LibraryMissing(f"{LIB_PATH} has ABI {L.xt_abi_version()}, expected {ABI_VERSION}; rebuild")
+    # the library must have been built from THIS tree's sources (xtddft_amd.build.source_hash)
+    from .build import source_hash
+    want, have = source_hash(), L.xt_build_id().decode()
+    if want is not None and have != want:
+        raise LibraryMissing(f"{LIB_PATH} was built from other sources (build id {have}, tree {want}); "
+                             f"run xtddft_amd.build.build()")
     _lib = L
     return L
 

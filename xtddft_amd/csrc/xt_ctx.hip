@@ -68,6 +68,7 @@ struct xt_ctx {
   int occ_basis[2] = {0, 0}, vir_basis[2] = {0, 0};
   double ck = 0.0, ck_lr = 0.0;
   bool has_orb = false, has_df = false, has_lr = false, has_grid = false, has_fock = false, has_eps = false;
+  bool has_vects = false;    // XSF OO basis set (empty for a doublet: no^2 - 1 = 0)
   DevBuf C, Bmo, Bmo_lr, Phi, kern, F, eps, vects;
   DevBuf ze, acc, kx, zr, tbuf, ubuf, gam, gam2, ws, stage, stage2, zin, sout, trace;
   DevBuf zp, accT, wbuf;
@@ -174,8 +175,8 @@ int xt_create(const xt_desc* desc, xt_ctx** out) {
   if (d.kind == XT_KIND_XTDA && d.si <= 0) return fail(XT_ERR_ARG, "XTDA needs spin > 0");
   if (d.kind == XT_KIND_XSF && d.sa > 0 && (d.no < 2 || !d.restricted))
     return fail(XT_ERR_ARG, "XSF spin adaptation needs ROKS with no >= 2 (2S-1 > 0)");
-  if (d.kind == XT_KIND_XSF && d.remove && d.no < 2)
-    return fail(XT_ERR_ARG, "XSF OO compression needs no >= 2");
+  if (d.kind == XT_KIND_XSF && d.remove && d.no < 1)
+    return fail(XT_ERR_ARG, "XSF OO compression needs an open shell");
   if (d.xctype < XT_XC_NONE || d.xctype > XT_XC_GGA) return fail(XT_ERR_ARG, "bad xctype");
   if ((d.kind == XT_KIND_SF_DOWN || d.kind == XT_KIND_SF_UP || d.kind == XT_KIND_XSF) && d.xctype == XT_XC_GGA)
     ; // ALDA0 uses densities only; the grid needs ao[0] only (SF_TDA.py:73-80)
@@ -493,10 +494,12 @@ int xt_set_grid(xt_ctx* c, const double* ao, const double* w, const double* kern
 }
 
 int xt_set_oo_basis(xt_ctx* c, const double* vects, int ptr_kind) {
-  if (!c || !vects) return fail(XT_ERR_ARG, "null argument");
+  if (!c || (!vects && c->d.no > 1)) return fail(XT_ERR_ARG, "null argument");
   (void)hipSetDevice(c->d.device);
   const size_t n = (size_t)c->d.no * c->d.no * (c->d.no * c->d.no - 1);
-  return to_device(c, c->vects, vects, n, ptr_kind);
+  if (n > 0) RET(to_device(c, c->vects, vects, n, ptr_kind));
+  c->has_vects = true;
+  return 0;
 }
 
 }  // extern "C"
@@ -1024,7 +1027,7 @@ extern "C" int xt_apply(xt_ctx* c, int nz, const double* z, double* sigma, int p
   const bool sf = d.kind == XT_KIND_SF_DOWN || d.kind == XT_KIND_SF_UP || xsf;
   if (d.add_local && d.kind != XT_KIND_UTDA && !c->has_fock) return fail(XT_ERR_STATE, "Fock matrices not set");
   if (d.add_local && d.kind == XT_KIND_UTDA && !c->has_eps) return fail(XT_ERR_STATE, "orbital energies not set");
-  if (xsf && d.remove && !c->vects.p) return fail(XT_ERR_STATE, "OO basis not set");
+  if (xsf && d.remove && !c->has_vects) return fail(XT_ERR_STATE, "OO basis not set");
   (void)hipSetDevice(d.device);
   const int O = c->O, V = c->V, nmo = d.nmo, nch = c->nchan;
   const long chs = (long)nz * O * V;
@@ -1166,7 +1169,8 @@ extern "C" int xt_xsf_j_diagonals(xt_ctx* c, double* co_j, double* ov_j, int ptr
   (void)hipSetDevice(c->d.device);
   const int nc = c->d.nc, no = c->d.no, nv = c->d.nv;
   RET(c->trace.ensure((size_t)nc * no + (size_t)no * nv));
-  xsf_jdiag(c->st, c->d.naux, c->d.nmo, nc, no, nv, c->Bmo.p, c->trace.p, c->trace.p + (size_t)nc * no);
+  // over this context's aux window (xt_set_partition): partial sums over ranks add up
+  xsf_jdiag(c->st, naux_w(c), c->d.nmo, nc, no, nv, bmo_of(c, c->Bmo, 0), c->trace.p, c->trace.p + (size_t)nc * no);
   const hipMemcpyKind k = ptr_kind == XT_PTR_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
   HIPCHK(hipMemcpyAsync(co_j, c->trace.p, (size_t)nc * no * 8, k, c->st));
   HIPCHK(hipMemcpyAsync(ov_j, c->trace.p + (size_t)nc * no, (size_t)no * nv * 8, k, c->st));
@@ -1185,7 +1189,13 @@ extern "C" int xt_dgemm(int transa, int transb, int m, int n, int k, double alph
   g.A = a; if (transa) { g.sAm = 1; g.sAk = lda; } else { g.sAm = lda; g.sAk = 1; }
   g.B = b; if (transb) { g.sBk = 1; g.sBn = ldb; } else { g.sBk = ldb; g.sBn = 1; }
   g.C = cc; g.ldc = ldc; g.alpha = alpha; g.beta = beta;
-  static thread_local DevBuf ws;
+  // split-K workspace per HIP device (the caller's current device owns the
+  // stream and the operands)
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  static thread_local std::vector<DevBuf> ws_dev;
+  if ((int)ws_dev.size() <= dev) ws_dev.resize(dev + 1);
+  DevBuf& ws = ws_dev[dev];
   size_t need = dgemm_workspace_bytes(g);
   if (need > 0) {
     size_t cap = (size_t)256 << 20;

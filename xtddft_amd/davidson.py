@@ -85,8 +85,9 @@ class _Dev:
     def gemm(self, ta, tb, m, n, k, alpha, a, lda, b, ldb, beta, c, ldc):
         if m == 0 or n == 0:
             return
-        _capi.check(self.L.xt_dgemm(ta, tb, m, n, k, alpha, a.data_ptr(), lda, b.data_ptr(), ldb,
-                                    beta, c.data_ptr(), ldc, ctypes.c_void_p(self.stream)), "xt_dgemm")
+        with self.torch.cuda.device(self.device):   # xt_dgemm keys its workspace by the current device
+            _capi.check(self.L.xt_dgemm(ta, tb, m, n, k, alpha, a.data_ptr(), lda, b.data_ptr(), ldb,
+                                        beta, c.data_ptr(), ldc, ctypes.c_void_p(self.stream)), "xt_dgemm")
 
     def norms2(self, x):
         out = self.torch.empty(x.shape[0], dtype=self.torch.float64, device=self.device)

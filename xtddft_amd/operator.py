@@ -238,6 +238,17 @@ class DeviceOperator:
 
     __call__ = apply
 
+    def apply_full(self, zs):
+        """The whole operator: this rank's partial sigma all-reduced over the
+        process group when the operator is sharded (what the drivers' vind
+        returns; ``apply`` is the rank-partial sum)."""
+        out = self.apply(zs)
+        if self.shard[1] > 1:
+            from .parallel import allreduce_sigma, require_group
+            require_group(self.shard[1])
+            out = allreduce_sigma(out)
+        return out
+
     def last_timings(self):
         buf = (ctypes.c_double * 4)()
         _capi.check(self._L.xt_last_timings(self._h, ctypes.cast(buf, ctypes.c_void_p)), "timings")
@@ -262,10 +273,17 @@ class DeviceOperator:
         return out
 
     def xsf_j_diagonals(self):
+        """XSF preconditioner J diagonals over this rank's aux rows, summed over
+        the group when sharded."""
         co = np.empty((self.nc, self.no))
         ov = np.empty((self.no, self.nv))
         _capi.check(self._L.xt_xsf_j_diagonals(self._h, co.ctypes.data, ov.ctypes.data,
                                                _capi.XT_PTR_HOST), "xt_xsf_j_diagonals")
+        if self.shard[1] > 1:
+            from .parallel import allreduce_sigma, require_group
+            require_group(self.shard[1])
+            both = allreduce_sigma(np.concatenate([co.ravel(), ov.ravel()]))
+            co, ov = both[:co.size].reshape(co.shape), both[co.size:].reshape(ov.shape)
         return co, ov
 
     def close(self):

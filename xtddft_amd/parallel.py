@@ -29,11 +29,37 @@ def shard_range(n: int, rank: int, nranks: int):
 
 
 def allreduce_sigma(sigma, group=None):
-    """In-place sum of the per-rank partial sigma (torch tensor)."""
+    """Sum of the per-rank partial sigma over the process group.
+
+    A torch tensor is reduced in place (through a host copy when the backend
+    is gloo and the tensor lives on the GPU); a NumPy array is reduced through
+    a CPU tensor and returned as a new array."""
+    import numpy as np
+    import torch
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(sigma, group=group)
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1):
+        return sigma
+    if isinstance(sigma, np.ndarray):
+        t = torch.from_numpy(np.ascontiguousarray(sigma, dtype=np.float64))
+        dist.all_reduce(t, group=group)
+        return t.numpy()
+    if sigma.is_cuda and dist.get_backend(group) == "gloo":
+        h = sigma.cpu()
+        dist.all_reduce(h, group=group)
+        sigma.copy_(h)
+        return sigma
+    dist.all_reduce(sigma, group=group)
     return sigma
+
+
+def require_group(nranks):
+    """A driver sharded over nranks > 1 needs the torch.distributed group that
+    sums its partial sigma; refuse to run on 1/nranks of the operator."""
+    import torch.distributed as dist
+    if nranks > 1 and not (dist.is_available() and dist.is_initialized()
+                           and dist.get_world_size() == nranks):
+        raise ValueError(f"shard over {nranks} ranks needs an initialised torch.distributed "
+                         f"group of that size (the partial sigma must be all-reduced)")
 
 
 class ShardedOperator:

@@ -20,6 +20,8 @@ import scipy.linalg
 from . import davidson as _dav
 from .meanfield import MeanField
 from .operator import DeviceOperator
+from .parallel import require_group
+from .utils import order_sf_down
 
 HA2EV = 27.2113834   # SF_TDA.py:15
 
@@ -51,25 +53,28 @@ def _collinear(mf):
     return m
 
 
-def gen_tda_operation_sf(mf, isf, method=0, device=0, shard=(0, 1)):
-    _check_method(method)
+def sf_hdiag(mf, isf):
+    """Orbital-energy gaps of the spin-flip space (SF_TDA.py:208-217)."""
     mo_energy, mo_occ, _ = mf_info(mf)
     occa = np.where(mo_occ[0] == 1)[0]; occb = np.where(mo_occ[1] == 1)[0]
     vira = np.where(mo_occ[0] == 0)[0]; virb = np.where(mo_occ[1] == 0)[0]
     if isf == -1:
-        hdiag = (mo_energy[1][virb, None] - mo_energy[0][occa]).T.ravel()
-        kind = 'SF_DOWN'
-    elif isf == 1:
-        hdiag = (mo_energy[0][vira, None] - mo_energy[1][occb]).T.ravel()
-        kind = 'SF_UP'
-    else:
-        raise ValueError("isf must be -1 (down) or +1 (up)")
+        return (mo_energy[1][virb, None] - mo_energy[0][occa]).T.ravel()
+    if isf == 1:
+        return (mo_energy[0][vira, None] - mo_energy[1][occb]).T.ravel()
+    raise ValueError("isf must be -1 (down) or +1 (up)")
+
+
+def gen_tda_operation_sf(mf, isf, method=0, device=0, shard=(0, 1)):
+    _check_method(method)
+    hdiag = sf_hdiag(mf, isf)
+    kind = 'SF_DOWN' if isf == -1 else 'SF_UP'
     op = DeviceOperator(_collinear(mf) if method == 2 else mf, kind, device=device, shard=shard)
 
     def vind(zs0):
         if isinstance(zs0, (list, tuple)):
             zs0 = np.asarray(zs0)
-        return op.apply(zs0)
+        return op.apply_full(zs0)
     vind.operator = op
     return vind, hdiag
 
@@ -90,12 +95,27 @@ def init_guess(mf, nstates, isf=-1):
     return x0
 
 
-def davidson_process(mf, nstates, method, isf=-1, device=0):
-    vind, hdiag = gen_tda_operation_sf(mf, isf, method, device=device)
+def _sf_shape(mf):
+    info = mf.shape_info()
+    return info['nc'], info['no'], info['nv']
+
+
+def deal_v_davidson(mf, v):
+    """Spin-flip-down eigenvectors (columns, PySCF occ_a x vir_b order) -> the
+    reference's cv|co|ov|oo block order (SF_TDA.py:304-345)."""
+    return np.asarray(v)[order_sf_down(*_sf_shape(mf))]
+
+
+def davidson_process(mf, nstates, method, isf=-1, device=0, shard=(0, 1), return_operator=False):
+    vind, hdiag = gen_tda_operation_sf(mf, isf, method, device=device, shard=shard)
     x0 = init_guess(mf, nstates, isf)
     conv, e, x1, icyc = _dav.davidson1(vind, x0, hdiag, tol=1e-7, lindep=1e-14, nroots=nstates,
                                        max_cycle=3000, device=device)
     v = np.array(x1).T
+    if isf == -1:   # SF_TDA.py:400-401
+        v = deal_v_davidson(mf, v)
+    if return_operator:
+        return e, v, conv, vind.operator
     return e, v, conv
 
 
@@ -106,30 +126,41 @@ def _dense(op):
         j1 = min(dim, j0 + 256)
         eye = np.zeros((j1 - j0, dim))
         eye[np.arange(j1 - j0), np.arange(j0, j1)] = 1.0
-        A[:, j0:j1] = op.apply(eye).T
+        A[:, j0:j1] = op.apply_full(eye).T
     return A
 
 
 class _SFBase:
     isf = 0
 
-    def __init__(self, mf, method=0, davidson=True, device=0):
+    def __init__(self, mf, method=0, davidson=True, device=0, shard=(0, 1)):
         _check_method(method)
         self.mf = mf
         self.method = method
         self.davidson = davidson
         self.device = device
-        info = mf.shape_info()
-        self.nc, self.no, self.nv = info['nc'], info['no'], info['nv']
+        self.shard = tuple(shard)
+        require_group(self.shard[1])
+        self.nc, self.no, self.nv = _sf_shape(mf)
+
+    def get_Amat(self):
+        """Explicit A through the device operator; SF-down in the reference's
+        cv|co|ov|oo block order (SF_TDA_down.get_Amat, SF_TDA.py:746-801)."""
+        vind, _ = gen_tda_operation_sf(self.mf, self.isf, self.method, device=self.device,
+                                       shard=self.shard)
+        A = _dense(vind.operator)
+        if self.isf == -1:
+            order = order_sf_down(self.nc, self.no, self.nv)
+            A = A[order][:, order]
+        return A
 
     def kernel(self, nstates=1):
         self.nstates = nstates
         if self.davidson:
-            self.e, self.v, self.converged = davidson_process(self.mf, nstates, self.method,
-                                                              self.isf, self.device)
+            self.e, self.v, self.converged, self._op = davidson_process(
+                self.mf, nstates, self.method, self.isf, self.device, self.shard, return_operator=True)
         else:
-            vind, _ = gen_tda_operation_sf(self.mf, self.isf, self.method, device=self.device)
-            self.A = _dense(vind.operator)
+            self.A = self.get_Amat()
             self.e, self.v = scipy.linalg.eigh(self.A)
         return self.e[:nstates] * HA2EV, self.v[:, :nstates]
 
@@ -141,10 +172,35 @@ class SF_TDA_up(_SFBase):
 class SF_TDA_down(_SFBase):
     isf = -1
 
+    def analyse(self, threshold=0.1, verbose=True):
+        """Delta<S^2> per root and dominant amplitudes from the cv|co|ov|oo
+        blocks (SF_TDA_down.analyse, SF_TDA.py:806-836; the <S^2> expression
+        holds for a ROKS reference)."""
+        nc, no, nv = self.nc, self.no, self.nv
+        d1, d2, d3 = nc * nv, nc * nv + nc * no, nc * nv + nc * no + no * nv
+        Ds, lines = [], []
+        for n in range(self.nstates):
+            value = np.asarray(self.v)[:, n]
+            cv = value[:d1].reshape(nc, nv)
+            co = value[d1:d2].reshape(nc, no)
+            ov = value[d2:d3].reshape(no, nv)
+            oo = value[d3:].reshape(no, no)
+            dp = (cv * cv).sum() - (oo * oo).sum() + np.trace(oo) ** 2
+            Ds.append(-no + 1 + dp)
+            lines.append(f'Excited state {n + 1} {self.e[n] * HA2EV:10.5f} eV D<S^2>={-no + 1 + dp:5.2f}')
+            for tag, blk, (o0, v0) in (('CV', cv, (0, nc + no)), ('CO', co, (0, nc)),
+                                       ('OV', ov, (nc, nc + no)), ('OO', oo, (nc, nc))):
+                for o, v in zip(*np.where(abs(blk) > threshold)):
+                    lines.append(f'{100 * blk[o, v] ** 2:3.0f}% {tag}(ab) {o + 1 + o0}a -> '
+                                 f'{v + 1 + v0}b {blk[o, v]:10.5f}')
+        if verbose:
+            print("\n".join(lines))
+        return Ds, lines
 
-def SF_TDA(mf, isf=-1, davidson=True, method=0, device=0):
+
+def SF_TDA(mf, isf=-1, davidson=True, method=0, device=0, shard=(0, 1)):
     if isf == -1:
-        return SF_TDA_down(mf, method, davidson, device)
+        return SF_TDA_down(mf, method, davidson, device, shard)
     if isf == 1:
-        return SF_TDA_up(mf, method, davidson, device)
+        return SF_TDA_up(mf, method, davidson, device, shard)
     raise ValueError("isf must be -1 or 1")

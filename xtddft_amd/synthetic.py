@@ -54,9 +54,12 @@ def grid_scale(ngrid, nocc, nvir, target=0.05):
 def make_df_tensor(rng, nao, naux, scale, decay=50.0):
     k = np.arange(nao)
     dmat = np.exp(-np.abs(k[:, None] - k[None, :]) / decay)
-    b = rng.standard_normal((naux, nao, nao))
-    b = (b + b.transpose(0, 2, 1)) * (scale / np.sqrt(2.0))
-    b *= dmat[None]
+    b = np.empty((naux, nao, nao))
+    # generated in P chunks (the same random stream as one draw) to bound the temporaries
+    pc = max(1, (1 << 28) // (8 * nao * nao))
+    for p0 in range(0, naux, pc):
+        t = rng.standard_normal((min(pc, naux - p0), nao, nao))
+        b[p0:p0 + t.shape[0]] = (t + t.transpose(0, 2, 1)) * (scale / np.sqrt(2.0)) * dmat[None]
     return b
 
 

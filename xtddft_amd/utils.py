@@ -28,6 +28,21 @@ def order_pyscf2my(nc: int, no: int, nv: int) -> np.ndarray:
     return np.concatenate([alpha, co, cv]).astype(np.int64)
 
 
+def order_sf_down(nc: int, no: int, nv: int) -> np.ndarray:
+    """Spin-flip-down vector order: PySCF's (occ_a x vir_b) row-major layout ->
+    the reference's cv|co|ov|oo blocks, block_vector = pyscf_vector[order]
+    (``deal_v_davidson``, SF_TDA.py:304-345; the explicit A of
+    SF_TDA_down.get_Amat is assembled in the same block order, SF_TDA.py:746-801)."""
+    vir = no + nv
+    rows_c = np.arange(nc)[:, None] * vir
+    rows_o = (nc + np.arange(no))[:, None] * vir
+    cv = (rows_c + no + np.arange(nv)[None, :]).ravel()
+    co = (rows_c + np.arange(no)[None, :]).ravel()
+    ov = (rows_o + no + np.arange(nv)[None, :]).ravel()
+    oo = (rows_o + np.arange(no)[None, :]).ravel()
+    return np.concatenate([cv, co, ov, oo]).astype(np.int64)
+
+
 def so2st(eigvec, nc, no, nv):
     """Spin-orbital -> spin-tensor basis for vectors stacked as columns."""
     cva = eigvec[:nc * nv]

@@ -25,6 +25,7 @@ import scipy.linalg
 from . import davidson as _dav
 from .meanfield import MeanField
 from .operator import DeviceOperator
+from .parallel import require_group
 from .sf_tda import _check_method, _dense, mf_info
 from .utils import HA2EV_XSF
 
@@ -83,7 +84,8 @@ class XSF_TDA:
         self.method = method
         self.collinear_samples = collinear_samples
         self.device = device
-        self.shard = shard
+        self.shard = tuple(shard)
+        require_group(self.shard[1])
         info = mf.shape_info()
         self.nc, self.no, self.nv = info['nc'], info['no'], info['nv']
         self.nocc_a, self.nocc_b = info['nocc_a'], info['nocc_b']
@@ -147,6 +149,7 @@ class XSF_TDA:
         if fglobal is None:
             fglobal = self.default_fglobal()
         op = self._operator(foo, fglobal)
+        self._op = op
         hdiag = self._build_preconditioner_hdiag(fglobal, op)
         if self.re:
             hdiag = self._compress_removed_hdiag(hdiag)
@@ -154,7 +157,7 @@ class XSF_TDA:
         def vind(zs0):
             if isinstance(zs0, (list, tuple)):
                 zs0 = np.asarray(zs0)
-            return op.apply(zs0)
+            return op.apply_full(zs0)
         vind.operator = op
         return vind, hdiag
 
@@ -221,8 +224,8 @@ class XSF_TDA:
         if frozen is not None:
             raise NotImplementedError("frozen-orbital XSF (frozen_A) is outside the hot path")
         self.re = (not self.type_u) if remove is None else bool(remove)
-        if self.re and self.no < 2:
-            raise ValueError("OO compression needs at least two open shells")
+        if self.re and self.no < 1:
+            raise ValueError("OO compression needs an open shell")
         nov = (self.nc + self.no) * (self.no + self.nv)
         self.nstates = min(nstates, nov)
         if fglobal is None:

@@ -19,6 +19,7 @@ import scipy.linalg
 from . import davidson as _dav
 from .meanfield import MeanField
 from .operator import DeviceOperator
+from .parallel import require_group
 from .utils import HA2EV, EVXNM, order_pyscf2my, so2st as _so2st
 
 CGS2AU = 1 / (235.7220 * 2)    # xtddft/utils/unit.py:9 (rotatory strength a.u. -> cgs)
@@ -42,7 +43,8 @@ class XTDA:
         self.lindep = LINDEP
         self.max_cycle = MAX_CYCLE
         self.device = device
-        self.shard = shard
+        self.shard = tuple(shard)
+        require_group(self.shard[1])
         if not isinstance(mf, MeanField):
             raise ValueError("mf must be a ROKS or UKS mean field")
         self.X = bool(mf.is_rohf)
@@ -95,7 +97,7 @@ class XTDA:
         def vind(zs):
             if isinstance(zs, (list, tuple)):
                 zs = np.asarray(zs)
-            return op.apply(zs)
+            return op.apply_full(zs)
         return vind, self._hdiag()
 
     def get_init_guess(self, mf=None, nstates=None, wfnsym=None, return_symmetry=False):
@@ -133,13 +135,11 @@ class XTDA:
         nc, no, nv = info['nc'], info['no'], info['nv']
         v = np.asarray(x1).T
         self.nc, self.no, self.nv = nc, no, nv
-        if self.X:
-            self.order = order_pyscf2my(nc, no, nv)
-            self.v = v[self.order, :]
-            self._split_blocks()
-            self.dS2 = self.deltaS2()
-        else:
-            self.v = v
+        # ROKS and UKS alike: "my order" and Delta<S^2> (XTDA.py:796-815)
+        self.order = order_pyscf2my(nc, no, nv)
+        self.v = v[self.order, :]
+        self._split_blocks()
+        self.dS2 = self.deltaS2()
         return self.e
 
     def full_diag(self):
@@ -152,21 +152,19 @@ class XTDA:
             j1 = min(dim, j0 + blk)
             eye = np.zeros((j1 - j0, dim))
             eye[np.arange(j1 - j0), np.arange(j0, j1)] = 1.0
-            A[:, j0:j1] = op.apply(eye).T
+            A[:, j0:j1] = op.apply_full(eye).T
         info = self.mf.shape_info()
         nc, no, nv = info['nc'], info['no'], info['nv']
         self.nc, self.no, self.nv = nc, no, nv
-        if self.X:
-            self.order = order_pyscf2my(nc, no, nv)
-            A = A[self.order][:, self.order]
+        self.order = order_pyscf2my(nc, no, nv)
+        A = A[self.order][:, self.order]
         self.A = A
         e, v = scipy.linalg.eigh(A)
         self.e = e[:self.nstates]
         self.e_eV = self.e * HA2EV
         self.v = v[:, :self.nstates]
-        if self.X:
-            self._split_blocks()
-            self.dS2 = self.deltaS2()
+        self._split_blocks()
+        self.dS2 = self.deltaS2()
         return self.e
 
     # ---------------------------------------------------------- properties
@@ -193,20 +191,29 @@ class XTDA:
             if mol is None or not hasattr(mol, "intor_symmetric"):
                 raise ValueError("osc_str needs AO dipole integrals: pass dipole_ao or a Mole with intor")
             dipole_ao = mol.intor_symmetric("int1e_r", comp=3)
-        mf = self.mf
-        c = mf.mo_coeff
-        occ_a = mf.mo_occ >= 1
-        vir_a = mf.mo_occ == 0
-        occ_b = mf.mo_occ >= 2
-        vir_b = mf.mo_occ != 2
-        da = np.einsum('xpq,pi,qj->xij', dipole_ao, c[:, occ_a], c[:, vir_a]).reshape(3, -1)
-        db = np.einsum('xpq,pi,qj->xij', dipole_ao, c[:, occ_b], c[:, vir_b]).reshape(3, -1)
-        nv = self.nv
-        na = (self.nc + self.no) * nv
-        db = db[:, self.order[na:] - na]
-        vt = self.v.T
-        tdip = np.einsum('xi,yi->yx', da, vt[:, :na]) + np.einsum('xi,yi->yx', db, vt[:, na:])
+        tdip = self._transition(dipole_ao)
         return 2. / 3. * np.einsum('s,sx,sx->s', self.e[:self.nstates], tdip, tdip)
+
+    def _spin_orbitals(self):
+        """(C_occ_a, C_vir_a, C_occ_b, C_vir_b): ROKS occupations >= 1 / >= 2
+        (XTDA.py:807-810); UKS per-spin coefficients."""
+        mf = self.mf
+        if self.X:
+            c = mf.mo_coeff
+            return (c[:, mf.mo_occ >= 1], c[:, mf.mo_occ == 0], c[:, mf.mo_occ >= 2], c[:, mf.mo_occ != 2])
+        ca, cb = mf.mo_coeff[0], mf.mo_coeff[1]
+        oa, ob = mf.mo_occ[0], mf.mo_occ[1]
+        return ca[:, oa > 0], ca[:, oa == 0], cb[:, ob > 0], cb[:, ob == 0]
+
+    def _transition(self, op_ao):
+        """<0|op|n> (n, 3) of a 3-component AO operator for the roots in self.v."""
+        coa, cva, cob, cvb = self._spin_orbitals()
+        a = np.einsum('xpq,pi,qj->xij', op_ao, coa, cva).reshape(3, -1)
+        b = np.einsum('xpq,pi,qj->xij', op_ao, cob, cvb).reshape(3, -1)
+        na = (self.nc + self.no) * self.nv
+        b = b[:, self.order[na:] - na]
+        vt = self.v.T
+        return np.einsum('xi,yi->yx', a, vt[:, :na]) + np.einsum('xi,yi->yx', b, vt[:, na:])
 
     def _qc_mol(self):
         mol = self.mol if hasattr(self.mol, "intor") else self.mf.extra.get("qc_mol")
@@ -223,21 +230,8 @@ class XTDA:
             mol = self._qc_mol()
             dip_ele_ao = mol.intor('int1e_ipovlp', comp=3, hermi=2)
             dip_meg_ao = mol.intor('int1e_cg_irxp', comp=3, hermi=2)
-        mf = self.mf
-        c = mf.mo_coeff
-        occ_a, vir_a = mf.mo_occ >= 1, mf.mo_occ == 0
-        occ_b, vir_b = mf.mo_occ >= 2, mf.mo_occ != 2
-        nv = self.nv
-        na = (self.nc + self.no) * nv
-        vt = self.v.T
-
-        def trans(op_ao):
-            a = np.einsum('xpq,pi,qj->xij', op_ao, c[:, occ_a], c[:, vir_a]).reshape(3, -1)
-            b = np.einsum('xpq,pi,qj->xij', op_ao, c[:, occ_b], c[:, vir_b]).reshape(3, -1)
-            b = b[:, self.order[na:] - na]
-            return np.einsum('xi,yi->yx', a, vt[:, :na]) + np.einsum('xi,yi->yx', b, vt[:, na:])
-        ele = -trans(dip_ele_ao)
-        meg = 0.5 * trans(dip_meg_ao)
+        ele = -self._transition(dip_ele_ao)
+        meg = 0.5 * self._transition(dip_meg_ao)
         omega = self.e[:self.nstates]
         return np.einsum('s,sx,sx->s', 1.0 / omega, ele, meg) / CGS2AU
 
