@@ -234,59 +234,89 @@ def _oracle_vind(args, mf):
         return osf.gen_tda_operation_sf(mf, 1 if args.kind == "SF_UP" else -1)
     o = oxsf.XSFOracle(mf, SA=args.sa)
     o.re = bool(args.remove)
+    if o.re and o.no > 1:
+        o.vects = oxsf.get_vect(o.no)
     return o.gen_tda_operation_sf(fglobal=0.7 * args.hyb + 0.3)
 
 
-def _time_call(f, reps):
+def log(msg):
+    """Progress to stderr (long phases must keep writing: the GPU box kills silent runs)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def _time_call(f, reps, what=""):
+    t0 = time.perf_counter()
     f()                                  # 1 warm-up (BASELINE.md 3)
+    log(f"cpu baseline {what}: warm-up {time.perf_counter() - t0:.2f} s")
     ts = []
     for _ in range(reps):
         t0 = time.perf_counter()
         f()
         ts.append(time.perf_counter() - t0)
+        log(f"cpu baseline {what}: {ts[-1]:.2f} s")
     return float(np.median(ts))
 
 
 def cpu_baseline(args):
     """The oracle's A.x (the reference's AO-route algorithm, NumPy/BLAS) on ALL
-    host cores, one trial vector per call, 1 warm-up + median of 5.
+    host cores, one trial vector per call.
 
-    Small shapes are timed at the full (naux, ngrid).  Large ones at the full
-    naux and two bounded grid sizes: the grid loop is blockwise, so t(ngrid)
-    is linear and only the grid dimension is extrapolated.  Returns matvecs/s."""
+    Shapes whose AO grid data stay small are timed at the full (naux, ngrid),
+    1 warm-up + median of 5.  The large ones: t = t_A + s (ngrid - g1) with t_A
+    timed at the FULL naux and ngrid g1 (1 warm-up + median of 3: ~10 s calls)
+    and the grid slope s from two grid sizes at a small naux (1 warm-up +
+    median of 5 each; the J/K work does not depend on the grid and the blockwise
+    grid loop is linear in ngrid), so only the grid dimension is extrapolated.
+    The exact-K configuration contracts stored 4-index ERIs (the incore
+    mf._eri route), built from the same factor.  Returns matvecs/s."""
+    import dataclasses
     from threadpoolctl import threadpool_info, threadpool_limits
-    from xtddft_amd.synthetic import as_eri8, make_mf, make_trial_vectors
+    from oracle.engines import eri_full_from_cderi
+    from xtddft_amd.synthetic import make_mf, make_trial_vectors
     ncpu = os.cpu_count() or 1
     t_all = time.perf_counter()
     with threadpool_limits(limits=ncpu):
         threads = max([i.get("num_threads", 1) for i in threadpool_info()
                        if i.get("user_api") == "blas"] or [1])
-        mkind = "RO"
+        log(f"cpu baseline on {threads} BLAS threads ({ncpu} host CPUs)")
 
-        def t_vec(ngrid):
-            mf = make_mf(nao=args.nao, nc=args.nc, no=args.no, naux=args.naux, ngrid=ngrid,
-                         xctype=args.xc, hyb=args.hyb, kind=mkind)
+        def build(naux, ngrid):
+            mf = make_mf(nao=args.nao, nc=args.nc, no=args.no, naux=naux, ngrid=ngrid,
+                         xctype=args.xc, hyb=args.hyb)
             if args.jk == "ERI8":
-                mf = as_eri8(mf)
+                mf = dataclasses.replace(mf, extra=dict(eri_full=eri_full_from_cderi(mf.cderi)))
+            return mf
+
+        def t_vec(mf, reps, what):
             vind, hdiag = _oracle_vind(args, mf)
             z = make_trial_vectors(1, hdiag.size)
-            return _time_call(lambda: vind(z), 5)
-        # full size when the AO-route grid data stay small (< 4 GB)
+            return _time_call(lambda: vind(z), reps, what)
         full = 8.0 * 4 * args.ngrid * args.nao < 4e9
         if full:
-            t = t_vec(args.ngrid)
-            how = f"measured at the full size (naux={args.naux}, ngrid={args.ngrid})"
+            t = t_vec(build(args.naux, args.ngrid), 5, "full size")
+            how = f"timed at the full size (naux={args.naux}, ngrid={args.ngrid}), 1 warm-up + median of 5"
         else:
-            g1, g2 = 8192, 24576
-            ta, tb = t_vec(g1), t_vec(g2)
-            slope = (tb - ta) / (g2 - g1)
-            t = ta + slope * (args.ngrid - g1)
-            how = (f"measured at the full naux={args.naux} with ngrid {g1} ({ta:.2f} s) and {g2} "
-                   f"({tb:.2f} s); linear in ngrid to {args.ngrid}")
+            g1, g2, n_small = 8192, 24576, 16
+            small = build(n_small, g1)
+            # full-naux factor: the small factor tiled (the BLAS work depends on the
+            # shape, not the values; avoids generating 8 naux nao^2 bytes of normals)
+            reps_ = -(-args.naux // n_small)
+            big = dataclasses.replace(small, cderi=np.tile(small.cderi, (reps_, 1, 1))[:args.naux]
+                                      * np.sqrt(n_small / args.naux))
+            t_a = t_vec(big, 3, f"naux={args.naux} ngrid={g1}")
+            del big
+            s1 = t_vec(small, 5, f"naux={n_small} ngrid={g1}")
+            s2 = t_vec(build(n_small, g2), 5, f"naux={n_small} ngrid={g2}")
+            slope = (s2 - s1) / (g2 - g1)
+            t = t_a + slope * (args.ngrid - g1)
+            how = (f"timed at the full naux={args.naux} with ngrid={g1} ({t_a:.2f} s, 1 warm-up + median "
+                   f"of 3) plus the grid slope {slope * 1e6:.3f} s per 1e6 points from ngrid {g1} / {g2} "
+                   f"at naux={n_small} ({s1:.3f} / {s2:.3f} s, 1 warm-up + median of 5); "
+                   f"extrapolated in ngrid only, to {args.ngrid}")
     return dict(value=1.0 / t, unit="matvecs/s", cores=int(threads), kind="port",
-                sample=(f"oracle {KIND_NAME[args.kind]} vind (NumPy AO route, {args.jk} J/K, {args.xc}) "
-                        f"on 1 vector at nao={args.nao}, {how}; 1 warm-up + median of 5; "
-                        f"t_vec = {t:.2f} s"),
+                sample=(f"oracle {KIND_NAME[args.kind]} vind (NumPy AO route, "
+                        f"{'stored 4-index ERI' if args.jk == 'ERI8' else 'DF'} J/K, {args.xc}) on 1 vector "
+                        f"at nao={args.nao}: {how}; t_vec = {t:.2f} s"),
                 host=_host_info(), sample_wall_s=round(time.perf_counter() - t_all, 1))
 
 
@@ -344,6 +374,7 @@ def converge(args, w, allreduce):
         stats["s"] += time.perf_counter() - t
         return s
     torch.cuda.synchronize()
+    log(f"converging {args.nroots} roots")
     tc = time.perf_counter()
     conv, e, _, icyc = davidson1(aop, x0, pre, nroots=args.nroots, device=dev.index,
                                  return_device=True, **kw)
@@ -421,8 +452,10 @@ def rank_main(args):
         if use_gpu:
             torch.cuda.synchronize()
 
+    log(f"rank {rank}/{world}: building the {args.config} workload")
     w = _factory()(args, rank, world, local)
     op = w.op
+    log(f"rank {rank}: generation {w.t_gen:.2f} s, operator construction {w.t_op:.2f} s")
     gen = torch.Generator(device=w.device)
     gen.manual_seed(20261016)
     z = torch.randn((args.nvec, op.dim), dtype=torch.float64, device=w.device, generator=gen)
@@ -455,6 +488,7 @@ def rank_main(args):
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     T = float(tt.item())
+    log(f"timed {args.steps} steps: {1e3 * T / args.steps:.2f} ms per step")
     verify = w.verify(z, out) if hasattr(w, "verify") else None   # a workload's own self-check
     phases = op.last_timings()
     roofline = roofline_of(args, stats_acc, args.steps)

@@ -53,8 +53,10 @@ def get_jk(cderi, dms, with_j=True, with_k=True):
         for x in range(d.shape[0]):
             for p0 in range(0, naux, pc):
                 b = cderi[p0:p0 + pc]
-                t = np.matmul(b, d[x])               # (pc, nao, nao): B_P D
-                vk[x] += np.einsum('pml,pln->mn', t, b, optimize=True)
+                # B_P D for the whole chunk as one GEMM, then sum_P (B_P D) B_P
+                t = (b.reshape(-1, nao) @ d[x]).reshape(b.shape)
+                for q in range(b.shape[0]):
+                    vk[x] += t[q] @ b[q]
         vk = vk.reshape(shape)
     return vj, vk
 
@@ -75,15 +77,50 @@ def unpack_eri_s8(packed, nao):
     return full
 
 
-def get_jk_eri(eri_full, dms, with_j=True, with_k=True):
+def get_jk_eri(eri_full, dms, with_j=True, with_k=True, eri_k=None):
     """PySCF incore get_jk convention on a full 4-index tensor:
-    vj = einsum('ijkl,kl->ij', eri, dm), vk = einsum('ijkl,jk->il', eri, dm)."""
+    vj = einsum('ijkl,kl->ij', eri, dm), vk = einsum('ijkl,jk->il', eri, dm),
+    as matrix products over the pair index (eri_k: the (i,l),(j,k) re-layout,
+    built here when not cached by the caller)."""
     dms = np.asarray(dms, dtype=np.float64)
     shape = dms.shape
-    d = dms.reshape(-1, shape[-2], shape[-1])
-    vj = np.einsum('ijkl,xkl->xij', eri_full, d).reshape(shape) if with_j else None
-    vk = np.einsum('ijkl,xjk->xil', eri_full, d).reshape(shape) if with_k else None
+    n = shape[-1]
+    d = dms.reshape(-1, n * n)
+    vj = vk = None
+    if with_j:
+        vj = (eri_full.reshape(n * n, n * n) @ d.T).T.reshape(shape)
+    if with_k:
+        if eri_k is None:
+            eri_k = eri_k_layout(eri_full)
+        vk = (eri_k @ d.T).T.reshape(shape)
     return vj, vk
+
+
+def eri_k_layout(eri_full):
+    """(i l),(j k) matrix of (ij|kl) for the exchange contraction."""
+    n = eri_full.shape[0]
+    return np.ascontiguousarray(eri_full.transpose(0, 3, 1, 2)).reshape(n * n, n * n)
+
+
+def eri_full_from_cderi(cderi):
+    """(ij|kl) = sum_P B[P,i,j] B[P,k,l] as a full 4-index array."""
+    naux, n, _ = cderi.shape
+    b = cderi.reshape(naux, n * n)
+    return (b.T @ b).reshape(n, n, n, n)
+
+
+def jk(mf, dms, with_j=True, with_k=True, lr=False):
+    """get_jk on the mean field's J/K model: stored 4-index ERIs when the caller
+    attached them (mf.extra['eri_full'], the incore mf._eri route), else the
+    DF factor."""
+    key = "eri_full_lr" if lr else "eri_full"
+    eri = mf.extra.get(key) if getattr(mf, "extra", None) else None
+    if eri is None:
+        return get_jk(mf.cderi_lr if lr else mf.cderi, dms, with_j, with_k)
+    kk = key + "_k"
+    if with_k and kk not in mf.extra:
+        mf.extra[kk] = eri_k_layout(eri)
+    return get_jk_eri(eri, dms, with_j, with_k, eri_k=mf.extra.get(kk))
 
 
 def get_k_total(mf, dms):
@@ -91,9 +128,9 @@ def get_k_total(mf, dms):
     c_full, c_lr = _k_coeffs(mf)
     vk = np.zeros_like(np.asarray(dms, dtype=np.float64))
     if c_full != 0:
-        vk += c_full * get_jk(mf.cderi, dms, with_j=False)[1]
+        vk += c_full * jk(mf, dms, with_j=False)[1]
     if c_lr != 0:
-        vk += c_lr * get_jk(mf.cderi_lr, dms, with_j=False)[1]
+        vk += c_lr * jk(mf, dms, with_j=False, lr=True)[1]
     return vk
 
 
@@ -167,18 +204,18 @@ def gen_response(mf, with_j=True):
     def vind(dm1):
         dm1 = np.asarray(dm1, dtype=np.float64)
         if mf.xctype == 'HF':
-            vj, vk = get_jk(mf.cderi, dm1)
+            vj, vk = jk(mf, dm1)
             return vj[0] + vj[1] - vk
         v1 = nr_uks_fxc(mf, dm1)
         hybrid = (mf.hyb != 0) or (mf.omega != 0)
         if not hybrid:
             if with_j:
-                vj = get_jk(mf.cderi, dm1, with_k=False)[0]
+                vj = jk(mf, dm1, with_k=False)[0]
                 v1 += vj[0] + vj[1]
             return v1
         vk = get_k_total(mf, dm1)
         if with_j:
-            vj = get_jk(mf.cderi, dm1, with_k=False)[0]
+            vj = jk(mf, dm1, with_k=False)[0]
             v1 += vj[0] + vj[1] - vk
         else:
             v1 -= vk
@@ -191,16 +228,16 @@ def gen_response_sf(mf, method=0):
     def vind(dm1):
         dm1 = np.asarray(dm1, dtype=np.float64)
         if mf.xctype == 'HF':
-            return -get_jk(mf.cderi, dm1, with_j=False)[1]
+            return -jk(mf, dm1, with_j=False)[1]
         if method == 0:
             v1 = nr_uks_fxc_sf_tda(mf, dm1)
         else:
             v1 = np.zeros_like(dm1)
         hybrid = (mf.hyb != 0) or (mf.omega != 0)
         if hybrid:
-            vk = mf.hyb * get_jk(mf.cderi, dm1, with_j=False)[1]
+            vk = mf.hyb * jk(mf, dm1, with_j=False)[1]
             if mf.omega > 1e-10:
-                vk += (mf.alpha - mf.hyb) * get_jk(mf.cderi_lr, dm1, with_j=False)[1]
+                vk += (mf.alpha - mf.hyb) * jk(mf, dm1, with_j=False, lr=True)[1]
             v1 -= vk
         return v1
     return vind

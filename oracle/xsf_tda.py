@@ -86,7 +86,7 @@ class XSFOracle:
                 trial[np.arange(idx.size), idx] = 1
                 trial = trial.reshape(idx.size, n_o, n_v)
                 dms = np.einsum("xov,qv,po->xpq", trial, orbv, orbo)
-                vj = engines.get_jk(self.mf.cderi, dms, with_k=False)[0]
+                vj = engines.jk(self.mf, dms, with_k=False)[0]
                 blk = np.einsum("xpq,pi,qu->xiu", vj, orbo, orbv).reshape(idx.size, n)
                 out[idx] = blk[np.arange(idx.size), idx]
             return out.reshape(n_o, n_v)
@@ -209,7 +209,7 @@ class XSFOracle:
                 dov = np.zeros_like(ov); doo = np.zeros_like(oo)
                 nb = cv.shape[0]
                 dm_hf = np.concatenate([d_cv, d_co, d_ov, d_oo], axis=0)
-                v1_j, v1_k = engines.get_jk(mf.cderi, dm_hf)
+                v1_j, v1_k = engines.jk(mf, dm_hf)
                 v1_cv_k = v1_k[:nb]
                 v1_co_j, v1_co_k = v1_j[nb:2 * nb], v1_k[nb:2 * nb]
                 v1_ov_j, v1_ov_k = v1_j[2 * nb:3 * nb], v1_k[2 * nb:3 * nb]

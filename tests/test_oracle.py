@@ -109,3 +109,19 @@ def test_golden_fixture_reproduced(case):
 def test_trial_vectors_normalised():
     z = make_trial_vectors(4, 50)
     assert np.allclose(np.linalg.norm(z, axis=1), 1.0)
+
+
+def test_oracle_stored_eri_route_equals_df():
+    """The oracle's incore-ERI J/K route (mf.extra['eri_full'], PySCF mf._eri
+    convention) gives the DF route's sigma for ERI = B^T B: the CPU baseline of
+    the exact-K configuration times it."""
+    import dataclasses
+    from oracle.engines import eri_full_from_cderi
+    mf = make_mf(nao=14, nc=3, no=2, naux=30, ngrid=500, xctype="GGA", hyb=0.3, omega=0.4, alpha=0.7)
+    vind, hdiag = oxtda.gen_tda_operation(mf)
+    m2 = dataclasses.replace(mf, extra=dict(eri_full=eri_full_from_cderi(mf.cderi),
+                                            eri_full_lr=eri_full_from_cderi(mf.cderi_lr)))
+    vind2, _ = oxtda.gen_tda_operation(m2)
+    z = make_trial_vectors(3, hdiag.size)
+    ref = vind(z)
+    assert np.abs(vind2(z) - ref).max() < 1e-12 * np.abs(ref).max()

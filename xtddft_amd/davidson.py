@@ -10,10 +10,13 @@ returning the 4-tuple ``(conv, e, x, icyc)`` its callers unpack
   O(space x dim) operation -- the heff rows (``_fill_heff_hermitian``), the
   Ritz vectors (``_gen_x0``), residuals, projections -- is an FP64-MFMA GEMM
   through ``xt_dgemm``; preconditioning and norms are device kernels.
-* ``_qr`` and ``_normalize_xt_`` orthogonalise with two passes of classical
-  Gram-Schmidt as GEMMs (CGS2) instead of the reference's vector-by-vector
-  modified Gram-Schmidt: equal in exact arithmetic, same drop rule
-  (``norm**2 > lindep``), numerically at least as stable.
+* ``_qr`` orthonormalises a block with two host round trips: Gram-Schmidt
+  on the host in the coefficient space of the Gram matrix (same order and
+  drop rule ``norm**2 > lindep`` as the reference's vector-by-vector
+  modified Gram-Schmidt), then one Cholesky-QR pass on the device;
+  ``_normalize_xt_`` projects out the subspace with two passes of classical
+  Gram-Schmidt as GEMMs (CGS2).  Equal in exact arithmetic to the
+  reference's orthogonalisation, orthogonal to round-off.
 * only the small ``heff`` (<= (max_space+nroots)^2) crosses to the host for
   ``scipy.linalg.eigh`` (Davidson.py:199), as in the reference.
 
@@ -113,20 +116,56 @@ class _Dev:
             self.gemm(0, 0, n, dim, space, -1.0, coef, space, xs, dim, 1.0, xt, dim)
 
 
+def _gram_gs(g, lindep):
+    """Gram-Schmidt in coefficient space: rows of C (kept x n) with C x
+    orthonormal, processing the rows of x in order and dropping a row whose
+    residual norm**2 <= lindep (PySCF _qr's rule) -- from the Gram matrix
+    g = x x^T alone."""
+    n = g.shape[0]
+    c = np.zeros((n, n))
+    kept = 0
+    for i in range(n):
+        r = np.zeros(n)
+        r[i] = 1.0
+        if kept:
+            prod = c[:kept] @ g[:, i]
+            r -= prod @ c[:kept]
+        nrm2 = float(r @ g @ r)
+        if nrm2 > lindep:
+            c[kept] = r / np.sqrt(nrm2)
+            kept += 1
+    return c[:kept]
+
+
 def _qr(dev, x, lindep):
-    """Orthonormalise the rows of x in order, dropping dependent ones (PySCF _qr)."""
+    """Orthonormalise the rows of x in order, dropping dependent ones (PySCF
+    _qr, Davidson.py:152,172).  Block form with two host round trips instead
+    of one per vector: the Gram matrix x x^T (device GEMM) drives Gram-Schmidt
+    on the host in coefficient space (same order, same drop rule), Q1 = C x on
+    the device, then one Cholesky-QR pass Q = L^-1 Q1 (L L^T = Q1 Q1^T)
+    restores orthogonality to round-off (CholQR2 pattern)."""
     torch = dev.torch
     n, dim = x.shape
-    q = torch.empty_like(x)
-    nv = 0
-    for i in range(n):
-        xi = x[i:i + 1].clone()
-        dev.project_out(xi, q, nv)
-        nrm2 = float(dev.norms2(xi)[0])
-        if nrm2 > lindep:
-            q[nv] = xi[0] / np.sqrt(nrm2)
-            nv += 1
-    return q[:nv]
+    if n == 0:
+        return x
+    x = x.contiguous()
+    g = torch.empty((n, n), dtype=torch.float64, device=dev.device)
+    dev.gemm(0, 1, n, n, dim, 1.0, x, dim, x, dim, 0.0, g, n)
+    c = _gram_gs(g.cpu().numpy(), lindep)
+    k = c.shape[0]
+    if k == 0:
+        return x[:0]
+    ct = torch.as_tensor(np.ascontiguousarray(c), device=dev.device)
+    q = torch.empty((k, dim), dtype=torch.float64, device=dev.device)
+    dev.gemm(0, 0, k, dim, n, 1.0, ct, n, x, dim, 0.0, q, dim)
+    g2 = torch.empty((k, k), dtype=torch.float64, device=dev.device)
+    dev.gemm(0, 1, k, k, dim, 1.0, q, dim, q, dim, 0.0, g2, k)
+    g2h = g2.cpu().numpy()
+    linv = scipy.linalg.solve_triangular(np.linalg.cholesky(0.5 * (g2h + g2h.T)), np.eye(k), lower=True)
+    lt = torch.as_tensor(np.ascontiguousarray(linv), device=dev.device)
+    out = torch.empty_like(q)
+    dev.gemm(0, 0, k, dim, k, 1.0, lt, k, q, dim, 0.0, out, dim)
+    return out
 
 
 def _sort_elast(elast, conv_last, vlast, v):
