@@ -204,9 +204,25 @@ def _factory():
 # ---------------------------------------------------------------------------
 # CPU baseline: the oracle on this host's cores
 # ---------------------------------------------------------------------------
+def cpu_share():
+    """CPUs this process may use: the affinity mask, capped by the cgroup CPU quota
+    (cpu.max) when one is set -- on a shared GPU box the quota, not os.cpu_count(),
+    is what BLAS threads can actually run on."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                quota, period = f.read().split()[:2]
+            if quota != "max":
+                n = min(n, max(1, int(float(quota) / float(period))))
+        except (OSError, ValueError):
+            pass
+    return n
+
+
 def _host_info():
     """CPU model and BLAS build of the host timing the CPU baseline."""
-    info = {"host_cpus": os.cpu_count()}
+    info = {"host_cpus": os.cpu_count(), "cpu_share": cpu_share()}
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
@@ -261,9 +277,12 @@ def cpu_baseline(args):
     """The oracle's A.x (the reference's AO-route algorithm, NumPy/BLAS) on ALL
     host cores, one trial vector per call.
 
-    Shapes whose AO grid data stay small are timed at the full (naux, ngrid),
-    1 warm-up + median of 5.  The large ones: t = t_A + s (ngrid - g1) with t_A
-    timed at the FULL naux and ngrid g1 (1 warm-up + median of 3: ~10 s calls)
+    Threads: every CPU this process may run on (``cpu_share``: the host's CPUs
+    capped by the cgroup quota of a shared GPU box; more BLAS threads than the
+    quota only oversubscribe it).  Shapes whose AO grid data stay small are timed
+    at the full (naux, ngrid), 1 warm-up + median of 5.  The large ones:
+    t = t_A + s (ngrid - g1) with t_A timed at the FULL naux and ngrid g1 (one
+    call of tens of seconds, after a warm-up of the same vind at a small naux)
     and the grid slope s from two grid sizes at a small naux (1 warm-up +
     median of 5 each; the J/K work does not depend on the grid and the blockwise
     grid loop is linear in ngrid), so only the grid dimension is extrapolated.
@@ -273,12 +292,13 @@ def cpu_baseline(args):
     from threadpoolctl import threadpool_info, threadpool_limits
     from oracle.engines import eri_full_from_cderi
     from xtddft_amd.synthetic import make_mf, make_trial_vectors
-    ncpu = os.cpu_count() or 1
+    ncpu = cpu_share()
     t_all = time.perf_counter()
     with threadpool_limits(limits=ncpu):
         threads = max([i.get("num_threads", 1) for i in threadpool_info()
                        if i.get("user_api") == "blas"] or [1])
-        log(f"cpu baseline on {threads} BLAS threads ({ncpu} host CPUs)")
+        log(f"cpu baseline on {threads} BLAS threads ({ncpu} CPUs in this process's share, "
+            f"{os.cpu_count()} on the host)")
 
         def build(naux, ngrid):
             mf = make_mf(nao=args.nao, nc=args.nc, no=args.no, naux=naux, ngrid=ngrid,
@@ -303,14 +323,20 @@ def cpu_baseline(args):
             reps_ = -(-args.naux // n_small)
             big = dataclasses.replace(small, cderi=np.tile(small.cderi, (reps_, 1, 1))[:args.naux]
                                       * np.sqrt(n_small / args.naux))
-            t_a = t_vec(big, 3, f"naux={args.naux} ngrid={g1}")
-            del big
+            vind_s, hd = _oracle_vind(args, small)
+            vind_s(make_trial_vectors(1, hd.size))          # warms BLAS threads and allocators
+            vind_b, _ = _oracle_vind(args, big)
+            z1 = make_trial_vectors(1, hd.size)
+            t0 = time.perf_counter()
+            vind_b(z1)
+            t_a = time.perf_counter() - t0
+            log(f"cpu baseline naux={args.naux} ngrid={g1}: {t_a:.2f} s")
+            del big, vind_b
             s1 = t_vec(small, 5, f"naux={n_small} ngrid={g1}")
             s2 = t_vec(build(n_small, g2), 5, f"naux={n_small} ngrid={g2}")
             slope = (s2 - s1) / (g2 - g1)
             t = t_a + slope * (args.ngrid - g1)
-            how = (f"timed at the full naux={args.naux} with ngrid={g1} ({t_a:.2f} s, 1 warm-up + median "
-                   f"of 3) plus the grid slope {slope * 1e6:.3f} s per 1e6 points from ngrid {g1} / {g2} "
+            how = (f"timed at the full naux={args.naux} with ngrid={g1} ({t_a:.2f} s, one call) plus the grid slope {slope * 1e6:.3f} s per 1e6 points from ngrid {g1} / {g2} "
                    f"at naux={n_small} ({s1:.3f} / {s2:.3f} s, 1 warm-up + median of 5); "
                    f"extrapolated in ngrid only, to {args.ngrid}")
     return dict(value=1.0 / t, unit="matvecs/s", cores=int(threads), kind="port",

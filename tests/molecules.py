@@ -48,3 +48,43 @@ def hf_scf(kind: str):
 @lru_cache(maxsize=None)
 def hf_meanfield(kind: str):
     return hf_scf(kind).to_meanfield()
+
+
+def spin_blocks(mfield):
+    """(C_occ, C_vir) per spin in the X-TDA / U-TDA vector convention
+    (ROKS: alpha occupied = mo_occ >= 1, beta occupied = mo_occ >= 2, XTDA.py:565-586)."""
+    import numpy as np
+    if mfield.is_rohf:
+        c = (mfield.mo_coeff, mfield.mo_coeff)
+        occ = (mfield.mo_occ >= 1, mfield.mo_occ >= 2)
+    else:
+        c = (mfield.mo_coeff[0], mfield.mo_coeff[1])
+        occ = (mfield.mo_occ[0] > 0, mfield.mo_occ[1] > 0)
+    return [(c[s][:, occ[s]], c[s][:, ~occ[s]]) for s in range(2)]
+
+
+def fd_xc_response(scf, mfield, z, eps=1e-5):
+    """XC part of sigma = A z from the SCF's own V_xc by central finite differences:
+    V1_s = d/de V_xc,s[D0 + e D1] with D1 the symmetrised transition density of z
+    (hermi=0 densities enter rho and grad rho only through D + D^T), Richardson
+    extrapolated from steps 2e and e (error O(e^4) + round-off), projected onto the
+    occupied-virtual block of each spin.  This is what nr_uks_fxc's contraction
+    (XTDA.py:514) must equal for the vxc that the reference's printed SCF energy
+    pins."""
+    import numpy as np
+    blocks = spin_blocks(mfield)
+    nov = [co.shape[1] * cv.shape[1] for co, cv in blocks]
+    d0 = scf._dm
+    out = np.empty_like(z)
+    for x in range(z.shape[0]):
+        parts = [z[x, :nov[0]], z[x, nov[0]:]]
+        d1 = np.array([np.einsum('ov,pv,qo->pq', parts[s].reshape(co.shape[1], cv.shape[1]), cv, co)
+                       for s, (co, cv) in enumerate(blocks)])
+        ds = 0.5 * (d1 + d1.transpose(0, 2, 1))
+
+        def fd(h):
+            return (scf._vxc(d0 + h * ds)[1] - scf._vxc(d0 - h * ds)[1]) / (2 * h)
+        v1 = (4.0 * fd(eps) - fd(2 * eps)) / 3.0
+        out[x] = np.concatenate([np.einsum('pq,qo,pv->ov', v1[s], co, cv).ravel()
+                                 for s, (co, cv) in enumerate(blocks)])
+    return out

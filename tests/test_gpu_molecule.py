@@ -121,3 +121,23 @@ def test_rotatory_strengths_of_mirror_images(torch):
     scale = np.abs(r1).max()
     assert scale > 1e-6
     assert np.abs(r1 + r2).max() <= 1e-4 * scale
+
+
+@pytest.mark.parametrize("kind", ["ROKS", "UKS"])
+def test_device_gga_xc_response_equals_fd_of_vxc(torch, kind):
+    """The device's fused GGA XC contraction (forward U / W, point kernel, back L / M)
+    against the finite-difference derivative of the SCF's V_xc (E_SCF pinned to the
+    reference to 1e-9 Ha): sigma_xc = A(fxc) z - A(0) z on the same operator."""
+    import dataclasses
+    from molecules import fd_xc_response, hf_scf
+    from xtddft_amd.operator import DeviceOperator
+    from xtddft_amd.synthetic import make_trial_vectors
+    scf, mf = hf_scf(kind), hf_meanfield(kind)
+    name = "XTDA" if kind == "ROKS" else "UTDA"
+    op1 = DeviceOperator(mf, name)
+    op0 = DeviceOperator(dataclasses.replace(mf, fxc=mf.fxc * 0.0), name)
+    z = make_trial_vectors(3, op1.dim)
+    got = op1.apply(z) - op0.apply(z)
+    ref = fd_xc_response(scf, mf, z)
+    for x in range(3):
+        assert np.abs(got[x] - ref[x]).max() < 1e-7 * np.abs(ref[x]).max()

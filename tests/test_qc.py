@@ -194,3 +194,27 @@ def test_chiral_mol():
     twisted = [[1, 0, 0], [0, 0, 0], [0, 0, 1.5], [0.5, 0.866, 1.5]]         # H-F-F-H, 60 deg
     assert chiral_mol(Geo(twisted, [1, 9, 9, 1]))
     assert not chiral_mol(Geo([[1, 0, 0], [0, 0, 0], [0, 0, 1.5], [-1, 0, 1.5]], [1, 9, 9, 1]))  # trans
+
+
+@pytest.mark.parametrize("kind", ["ROKS", "UKS"])
+def test_oracle_gga_xc_response_equals_fd_of_vxc(kind):
+    """The oracle's nr_uks_fxc restatement (GGA, hermi=0) equals the finite-difference
+    derivative of the SCF's V_xc -- whose energy matches the reference's printed
+    E_SCF -- on the BHandHLYP HF molecule: the second-derivative kernel as
+    contracted is pinned through a pinned quantity (tolerance from the FD step)."""
+    from molecules import fd_xc_response, hf_meanfield, hf_scf, spin_blocks
+    from oracle import engines
+    from xtddft_amd.synthetic import make_trial_vectors
+    scf, mf = hf_scf(kind), hf_meanfield(kind)
+    blocks = spin_blocks(mf)
+    nov = [co.shape[1] * cv.shape[1] for co, cv in blocks]
+    z = make_trial_vectors(2, sum(nov))
+    ref = fd_xc_response(scf, mf, z)
+    for x in range(2):
+        parts = [z[x, :nov[0]], z[x, nov[0]:]]
+        d1 = np.array([np.einsum('ov,pv,qo->pq', parts[s].reshape(co.shape[1], cv.shape[1]), cv, co)
+                       for s, (co, cv) in enumerate(blocks)])
+        v1 = engines.nr_uks_fxc(mf, d1[:, None])[:, 0]
+        got = np.concatenate([np.einsum('pq,qo,pv->ov', v1[s], co, cv).ravel()
+                              for s, (co, cv) in enumerate(blocks)])
+        assert np.abs(got - ref[x]).max() < 1e-7 * np.abs(ref[x]).max()

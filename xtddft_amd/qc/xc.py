@@ -15,11 +15,21 @@ to round-off, no finite differences).  Forms follow libxc 7.0's definitions:
                     x_s = |grad rho_s| / rho_s^(4/3), beta = 0.0042
 * LYP correlation   Miehlich-Savin-Stoll-Preuss form (CPL 157, 200 (1989)),
                     a = 0.04918, b = 0.132, c = 0.2533, d = 0.349
+* VWN correlation   Vosko-Wilk-Nusair, Can. J. Phys. 58, 1200 (1980):
+                    VWN5 (libxc LDA_C_VWN: paramagnetic / ferromagnetic / spin
+                    stiffness fits, e = e_P + a_c f(z)(1 - z^4)/f''(0) + (e_F - e_P) f(z) z^4)
+                    and VWN_RPA (libxc LDA_C_VWN_RPA: the RPA fits interpolated by
+                    f(z) alone, e = e_P (1 - f(z)) + e_F f(z)).
 
 Hybrids: BHandHLYP = 0.5 HF + 0.5 B88 + LYP (libxc HYB_GGA_XC_BHANDHLYP), the
 reference's functional in every stored example (``example/XSF_TDA.ipynb``,
-``spin up.ipynb``); BLYP; HF (no DFT part).  Points whose total density is
-below ``DENS_THRESHOLD`` contribute nothing (libxc's density screening).
+``spin up.ipynb``); B3LYP = 0.2 HF + 0.08 Slater + 0.72 B88 + 0.19 VWN_RPA +
+0.81 LYP (libxc HYB_GGA_XC_B3LYP, which PySCF >= 2.3 calls B3LYP: the
+reference's default functional, XTDA.py:1526, and the one of example/TDA.ipynb)
+and B3LYP5 (same with VWN5); BLYP; SVWN (Slater + VWN5); HF (no DFT part).
+Points whose total density is below ``DENS_THRESHOLD`` contribute nothing
+(libxc's density screening).  The stored reference outputs pin BHandHLYP only
+(B3LYP's example needs cc-pVDZ, not available offline): VWN is unpinned.
 """
 from __future__ import annotations
 
@@ -38,6 +48,10 @@ _FUNCTIONALS = {
     "B88": ([("b88", 1.0)], 0.0, "GGA"),
     "BLYP": ([("b88", 1.0), ("lyp", 1.0)], 0.0, "GGA"),
     "BHANDHLYP": ([("b88", 0.5), ("lyp", 1.0)], 0.5, "GGA"),
+    "SVWN": ([("slater", 1.0), ("vwn5", 1.0)], 0.0, "LDA"),
+    "B3LYP": ([("slater", 0.08), ("b88", 0.72), ("vwn_rpa", 0.19), ("lyp", 0.81)], 0.2, "GGA"),
+    "B3LYPG": ([("slater", 0.08), ("b88", 0.72), ("vwn_rpa", 0.19), ("lyp", 0.81)], 0.2, "GGA"),
+    "B3LYP5": ([("slater", 0.08), ("b88", 0.72), ("vwn5", 0.19), ("lyp", 0.81)], 0.2, "GGA"),
 }
 
 
@@ -105,7 +119,48 @@ def _lyp(ra, rb, saa, sab, sbb, torch):
     return t1 - a * b * omega * br
 
 
-_PIECES = {"slater": _slater, "b88": _b88, "lyp": _lyp}
+# VWN fits (A in Hartree): index 0 paramagnetic, 1 ferromagnetic, 2 spin stiffness
+_VWN5 = dict(A=(0.0310907, 0.01554535, -1.0 / (6.0 * math.pi ** 2)), b=(3.72744, 7.06042, 1.13107),
+             c=(12.9352, 18.0578, 13.0045), x0=(-0.10498, -0.32500, -0.0047584))
+_VWN_RPA = dict(A=(0.0310907, 0.01554535, -1.0 / (6.0 * math.pi ** 2)), b=(13.0720, 20.1231, 1.06835),
+                c=(42.7198, 101.578, 11.4813), x0=(-0.409286, -0.743294, -0.228344))
+_FPP = 4.0 / (9.0 * (2.0 ** (1.0 / 3.0) - 1.0))           # f''(0)
+
+
+def _vwn_fit(prm, i, x, torch):
+    """VWN interpolation formula (eq. 4.4 of the paper) in x = sqrt(rs)."""
+    A, b, c, x0 = prm["A"][i], prm["b"][i], prm["c"][i], prm["x0"][i]
+    q = math.sqrt(4.0 * c - b * b)
+    X = x * x + b * x + c
+    X0 = x0 * x0 + b * x0 + c
+    at = torch.atan(q / (2.0 * x + b))
+    return A * (torch.log(x * x / X) + 2.0 * b / q * at
+                - b * x0 / X0 * (torch.log((x - x0) ** 2 / X) + 2.0 * (b + 2.0 * x0) / q * at))
+
+
+def _vwn_parts(ra, rb, torch):
+    rho = ra + rb
+    x = (3.0 / (4.0 * math.pi * rho)) ** (1.0 / 6.0)
+    z = (ra - rb) / rho
+    fz = ((1.0 + z) ** (4.0 / 3.0) + (1.0 - z) ** (4.0 / 3.0) - 2.0) / (2.0 ** (4.0 / 3.0) - 2.0)
+    return rho, x, z, fz
+
+
+def _vwn5(ra, rb, saa, sab, sbb, torch):
+    rho, x, z, fz = _vwn_parts(ra, rb, torch)
+    ep, ef = _vwn_fit(_VWN5, 0, x, torch), _vwn_fit(_VWN5, 1, x, torch)
+    ac = _vwn_fit(_VWN5, 2, x, torch)
+    z4 = z ** 4
+    return rho * (ep + ac * fz * (1.0 - z4) / _FPP + (ef - ep) * fz * z4)
+
+
+def _vwn_rpa(ra, rb, saa, sab, sbb, torch):
+    rho, x, z, fz = _vwn_parts(ra, rb, torch)
+    ep, ef = _vwn_fit(_VWN_RPA, 0, x, torch), _vwn_fit(_VWN_RPA, 1, x, torch)
+    return rho * (ep * (1.0 - fz) + ef * fz)
+
+
+_PIECES = {"slater": _slater, "b88": _b88, "lyp": _lyp, "vwn5": _vwn5, "vwn_rpa": _vwn_rpa}
 
 
 def eval_xc_eff(xc: str, rho: np.ndarray, deriv: int = 1):
