@@ -218,3 +218,103 @@ def test_oracle_gga_xc_response_equals_fd_of_vxc(kind):
         got = np.concatenate([np.einsum('pq,qo,pv->ov', v1[s], co, cv).ravel()
                               for s, (co, cv) in enumerate(blocks)])
         assert np.abs(got - ref[x]).max() < 1e-7 * np.abs(ref[x]).max()
+
+
+def test_basis_parser_nwchem_format():
+    """NWChem-format text (PySCF gto.basis.parse) reproduces the embedded 6-31G shells."""
+    from xtddft_amd.qc.basis import BASIS, parse_nwchem
+    text = """
+    # 6-31G hydrogen and fluorine, NWChem format
+    BASIS "ao basis" PRINT
+    H    S
+         18.731137   0.0334946
+          2.8253937  0.23472695
+          0.6401217  0.81375733
+    H    S
+          0.1612778  1.0
+    F    S
+       7001.71309    0.0018196169
+       1051.36609    0.0139160796
+        239.28569    0.0684053245
+         67.3974453  0.23318576
+         21.5199573  0.471267439
+          7.4031013  0.356618546
+    F    SP
+         20.8479528  -0.108506975  0.0716287243
+          4.80830834 -0.146451658  0.345912103
+          1.34406986  1.12868858   0.722469957
+    F    SP
+          0.358151393 1.0  1.0
+    END
+    """
+    got = parse_nwchem(text)
+    ref = BASIS["6-31g"]
+    assert got["H"] == ref["H"]
+    # PySCF orders the F shells s, s, s, p, p; the SP blocks interleave s and p
+    by_l = lambda shells: sorted(shells, key=lambda s: s[0])
+    assert by_l(got["F"]) == by_l(ref["F"])
+
+
+def test_three_index_integrals_match_four_index_routine():
+    """(ab|P) and (P|Q) (density fitting) against the 4-index McMurchie-Davidson
+    routine with the unit s function exp(0 r^2) as the partner (l_a, l_b <= 2,
+    aux l <= 4), on random shells and centres."""
+    from xtddft_amd.qc.gto import Shell
+    from xtddft_amd.qc.ints import AuxShellSet, ShellPair, eri2c, eri3c, eri_quartet
+    rng = np.random.default_rng(1)
+
+    def shell(l, c):
+        return Shell(0, l, np.array(c), rng.uniform(0.2, 3.0, 2), rng.uniform(0.5, 1.5, 2))
+
+    def unit(c):
+        return Shell(0, 0, np.asarray(c, dtype=float), np.array([0.0]), np.array([1.0]))
+    for la in range(3):
+        for lb in range(3):
+            for lc in range(5):
+                a, b = shell(la, [0.1, 0.2, -0.3]), shell(lb, [0.5, -0.4, 0.9])
+                cs = [shell(lc, [-0.7, 0.3, 0.2]), shell(lc, [0.2, 0.8, -0.5])]
+                pair = ShellPair(a, b)
+                got = eri3c(pair, AuxShellSet(cs))
+                for k, c in enumerate(cs):
+                    ref = eri_quartet(pair, ShellPair(c, unit(c.center)))[:, :, :, 0]
+                    assert np.abs(got[:, :, k, :] - ref).max() < 1e-12 * max(1, np.abs(ref).max())
+                g2 = eri2c(AuxShellSet(cs), AuxShellSet([a]))
+                ref2 = eri_quartet(ShellPair(cs[1], unit(cs[1].center)), ShellPair(a, unit(a.center)))[:, 0, :, 0]
+                assert np.abs(g2[1, :, 0, :] - ref2).max() < 1e-12 * max(1, np.abs(ref2).max())
+
+
+def test_solid_harmonics_are_harmonic():
+    """The l = 2..5 spherical transforms are harmonic polynomials (zero Laplacian)."""
+    from xtddft_amd.qc.gto import _solid_harmonics
+    from xtddft_amd.qc.ints import cart_comps
+    for l in range(2, 6):
+        t = _solid_harmonics(l)
+        assert np.linalg.matrix_rank(t) == 2 * l + 1
+        lower = {c: i for i, c in enumerate(cart_comps(l - 2))}
+        for row in t:
+            lap = np.zeros(len(lower))
+            for coef, (i, j, k) in zip(row, cart_comps(l)):
+                for d, e in ((0, i), (1, j), (2, k)):
+                    if e >= 2:
+                        c = [i, j, k]
+                        c[d] -= 2
+                        lap[lower[tuple(c)]] += coef * e * (e - 1)
+            assert np.abs(lap).max() < 1e-12
+
+
+def test_density_fitted_scf():
+    """mf.density_fit(): the fitted ERIs approximate the exact ones and the DF
+    ROKS energy stays within 1e-5 Ha of the exact-ERI energy the reference printed."""
+    from molecules import HF_IRREP_NELEC, hf_mol
+    from xtddft_amd.qc import ROKS
+    from xtddft_amd.qc.df import DF
+    mol = hf_mol()
+    b = DF(mol).build().cderi
+    assert np.abs(np.einsum('pij,pkl->ijkl', b, b) - mol.eri_full()).max() < 5e-4
+    mf = ROKS(mol, "bhandhlyp").density_fit()
+    mf.irrep_nelec = dict(HF_IRREP_NELEC)
+    mf.conv_tol = 1e-10
+    mf.kernel()
+    assert abs(mf.e_tot - reference_outputs()["roks_bhandhlyp_e_tot"]) < 1e-5
+    m = mf.to_meanfield()
+    assert m.jk_mode == "DF" and m.eri is None and m.naux == b.shape[0]

@@ -3,7 +3,8 @@
 Only data that the reference itself records is embedded: the 6-31G shells of
 F and H exactly as PySCF 2.12.1 printed them in the reference's example run
 (``example/XSF_TDA.ipynb``, cell 1 output, "[INPUT] ---- BASIS SET ----").
-Any other basis is passed to ``Mole`` as a dict in the same format.
+Any other basis is passed to ``Mole`` as a dict in the same format, or as
+NWChem-format text through ``parse_nwchem`` (PySCF ``gto.basis.parse``).
 """
 from __future__ import annotations
 
@@ -49,3 +50,44 @@ def load(name_or_dict, symbol: str):
     if symbol not in table:
         raise KeyError(f"basis {name_or_dict!r} has no data for {symbol} here")
     return table[symbol]
+
+
+_L = {"S": 0, "P": 1, "D": 2, "F": 3, "G": 4, "H": 5}
+
+
+def parse_nwchem(text: str, symbol: str | None = None):
+    """NWChem-format basis text -> {element: shells} (PySCF ``gto.basis.parse``).
+
+    Each block starts with ``<Element> <L>`` (L in S P D F G H, or ``SP`` for a
+    shared-exponent s+p pair) followed by rows ``exponent c1 [c2 ...]``; lines
+    starting with ``#`` and ``BASIS`` / ``END`` markers are ignored.  With
+    ``symbol`` the shells of that element are returned directly."""
+    out: dict = {}
+    cur = None
+    for raw in text.splitlines():
+        line = raw.split("#")[0].strip()
+        if not line or line.upper().startswith(("BASIS", "END")):
+            continue
+        f = line.split()
+        if f[0][0].isalpha():
+            el = f[0].capitalize()
+            lab = f[1].upper()
+            if lab == "SP":
+                cur = (el, "SP", [[0], [1]])
+                out.setdefault(el, []).extend(cur[2])
+            else:
+                shell = [_L[lab]]
+                cur = (el, lab, [shell])
+                out.setdefault(el, []).append(shell)
+            continue
+        if cur is None:
+            raise ValueError(f"basis data before a shell header: {raw!r}")
+        vals = [float(x.replace("D", "E").replace("d", "e")) for x in f]
+        if cur[1] == "SP":
+            cur[2][0].append([vals[0], vals[1]])
+            cur[2][1].append([vals[0], vals[2]])
+        else:
+            cur[2][0].append(vals)
+    if symbol is not None:
+        return out[symbol.capitalize()]
+    return out

@@ -25,7 +25,7 @@ from typing import List, Sequence
 import numpy as np
 
 from . import basis as _basis
-from .ints import ShellPair, cart_comps, eri_quartet
+from .ints import AuxShellSet, ShellPair, cart_comps, eri2c, eri3c, eri_quartet
 
 BOHR = 0.52917721092
 
@@ -38,21 +38,38 @@ C2V_IRREPS = ("A1", "A2", "B1", "B2")     # PySCF order; B1 ~ x, B2 ~ y
 
 
 def _sph_transform(l: int) -> np.ndarray:
-    """(n_sph, n_cart) un-normalised real solid harmonics in libcint order."""
+    """(n_sph, n_cart) un-normalised real solid harmonics in libcint order:
+    p as (x, y, z); l >= 2 as m = -l..l (d: xy, yz, z^2, xz, x^2-y^2), each the
+    Helgaker-Joergensen-Olsen expansion (eq. 6.4.48) of S_lm in Cartesian
+    monomials x^i y^j z^k (the AO normalisation is applied afterwards)."""
     if l == 0:
         return np.ones((1, 1))
     if l == 1:
         return np.eye(3)
-    if l == 2:
-        # cart order: xx xy xz yy yz zz
-        return np.array([
-            [0, 1, 0, 0, 0, 0],          # xy
-            [0, 0, 0, 0, 1, 0],          # yz
-            [-1, 0, 0, -1, 0, 2],        # 2zz - xx - yy
-            [0, 0, 1, 0, 0, 0],          # xz
-            [1, 0, 0, -1, 0, 0],         # xx - yy
-        ], dtype=np.float64)
-    raise NotImplementedError("shells with l > 2 are not supported")
+    return _solid_harmonics(l)
+
+
+def _solid_harmonics(l: int) -> np.ndarray:
+    from math import comb
+    comps = cart_comps(l)
+    pos = {c: i for i, c in enumerate(comps)}
+    out = np.zeros((2 * l + 1, len(comps)))
+    for row, m in enumerate(range(-l, l + 1)):
+        am = abs(m)
+        vm2 = 0 if m >= 0 else 1                     # 2 v_m
+        for t in range((l - am) // 2 + 1):
+            for u in range(t + 1):
+                # v = v_m .. floor(|m|/2 - v_m) + v_m, stored as 2v
+                v2 = vm2
+                while v2 <= 2 * ((am - vm2) // 2) + vm2 and v2 <= am:
+                    c = ((-1) ** (t + (v2 - vm2) // 2) * 0.25 ** t * comb(l, t) * comb(l - t, am + t)
+                         * comb(t, u) * comb(am, v2))
+                    ix = 2 * t + am - 2 * u - v2
+                    iy = 2 * u + v2
+                    iz = l - 2 * t - am
+                    out[row, pos[(ix, iy, iz)]] += c
+                    v2 += 2
+    return out
 
 
 def gto_norm(l: int, a: np.ndarray) -> np.ndarray:
@@ -255,6 +272,56 @@ class Mole:
         if key == "int2e":
             return self.eri_full()
         raise KeyError(name)
+
+    # -------------------------------------------------- density fitting
+    def _aux_groups(self):
+        """{l: (AuxShellSet, AO offsets of its shells)} in shell order."""
+        groups = {}
+        for k, sh in enumerate(self.shells):
+            groups.setdefault(sh.l, []).append(k)
+        return {l: (AuxShellSet([self.shells[k] for k in ks]), [int(self.ao_loc[k]) for k in ks])
+                for l, ks in groups.items()}
+
+    def int3c2e(self, auxmol) -> np.ndarray:
+        """(P|mu nu) over normalised spherical functions: (naux, nao, nao) -- PySCF
+        ``df.incore.aux_e2(mol, auxmol, 'int3c2e')`` transposed to aux-major."""
+        n, naux = self._nao, auxmol.nao
+        out = np.zeros((naux, n, n))
+        aux = auxmol._aux_groups()
+        Ta = {l: _sph_transform(l) for l in aux}
+        sh = self.shells
+        for i in range(len(sh)):
+            Ti = _sph_transform(sh[i].l)
+            a = slice(self.ao_loc[i], self.ao_loc[i + 1])
+            for j in range(i + 1):
+                Tj = _sph_transform(sh[j].l)
+                b = slice(self.ao_loc[j], self.ao_loc[j + 1])
+                pair = ShellPair(sh[i], sh[j])
+                for l, (aset, offs) in aux.items():
+                    blk = eri3c(pair, aset)                          # (ca, cb, k, cP)
+                    blk = np.einsum('mi,nj,ijkc,pc->kpmn', Ti, Tj, blk, Ta[l], optimize=True)
+                    for k, o in enumerate(offs):
+                        out[o:o + 2 * l + 1, a, b] = blk[k]
+                        out[o:o + 2 * l + 1, b, a] = blk[k].transpose(0, 2, 1)
+        nrm = self._norm
+        out *= auxmol._norm[:, None, None] * nrm[None, :, None] * nrm[None, None, :]
+        return out
+
+    def int2c2e(self) -> np.ndarray:
+        """(P|Q) of this (auxiliary) basis over normalised spherical functions."""
+        n = self._nao
+        out = np.zeros((n, n))
+        groups = self._aux_groups()
+        for la, (sa, oa) in groups.items():
+            for lb, (sb, ob) in groups.items():
+                blk = eri2c(sa, sb)                                  # (ka, ca, kb, cb)
+                blk = np.einsum('pa,kalc,qc->kplq', _sph_transform(la), blk, _sph_transform(lb),
+                                optimize=True)
+                for k, o1 in enumerate(oa):
+                    for m, o2 in enumerate(ob):
+                        out[o1:o1 + 2 * la + 1, o2:o2 + 2 * lb + 1] = blk[k, :, m, :]
+        nrm = self._norm
+        return out * (nrm[:, None] * nrm[None, :])
 
     def eri_full(self) -> np.ndarray:
         """(mu nu|la si) over normalised spherical AOs, all 8 symmetry copies filled."""

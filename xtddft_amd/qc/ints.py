@@ -305,3 +305,71 @@ def eri_quartet(bra: ShellPair, ket: ShellPair) -> np.ndarray:
     Rm = R[idx] * pref                                                 # (ntab, ntcd, P, Q)
     X = np.einsum('tsPQ,s,cdsQ->tcdP', Rm, sign, ket.Eab, optimize=True)
     return np.einsum('abtP,tcdP->abcd', bra.Eab, X, optimize=True)
+
+
+# ------------------------------------------------------------ 3-index (DF)
+class AuxShellSet:
+    """All auxiliary shells of one angular momentum, primitives stacked (for the
+    3-index Coulomb integrals (ab|P) of density fitting).
+
+    Each primitive of shell k is a one-centre Hermite expansion (the ket of a
+    pair whose second function is the unit s function exp(0 r^2)); ``seg``
+    maps stacked primitives to shells so the contraction is one product."""
+
+    def __init__(self, shells):
+        self.l = shells[0].l
+        self.shells = shells
+        self.p = np.concatenate([s.exps for s in shells])
+        self.P = np.concatenate([np.repeat(s.center[None], s.exps.size, 0) for s in shells])
+        self.coef = np.concatenate([s.coefs for s in shells])
+        self.seg = np.zeros((self.p.size, len(shells)))
+        q = 0
+        for k, s in enumerate(shells):
+            self.seg[q:q + s.exps.size, k] = 1.0
+            q += s.exps.size
+        # one-centre Hermite coefficients E^{i0}_t (b = 0): x^i e^{-p x^2} = sum_t E_t Lambda_t
+        l = self.l
+        tuv, _ = hermite_index(l)
+        E1 = hermite_e(l, 0, self.p, np.zeros_like(self.p), 0.0)       # (l+1, 1, l+1, Q)
+        comps = cart_comps(l)
+        Ek = np.zeros((len(comps), len(tuv), self.p.size))
+        for i, (ax, ay, az) in enumerate(comps):
+            for k, (t, u, v) in enumerate(tuv):
+                if t > ax or u > ay or v > az:
+                    continue
+                Ek[i, k] = E1[ax, 0, t] * E1[ay, 0, u] * E1[az, 0, v] * self.coef
+        self.Ek = Ek
+
+
+def eri3c(bra: ShellPair, aux: AuxShellSet) -> np.ndarray:
+    """(ab|P) over Cartesian components for every shell of ``aux``:
+    (nca, ncb, nshell_aux, ncart_aux)."""
+    p = bra.p[:, None]
+    q = aux.p[None, :]
+    alpha = p * q / (p + q)
+    d = bra.P[:, None, :] - aux.P[None, :, :]
+    L = bra.L + aux.l
+    R = hermite_r(L, alpha, d[..., 0], d[..., 1], d[..., 2])          # (ntuv_L, P, Q)
+    pref = 2.0 * np.pi ** 2.5 / (p * q * np.sqrt(p + q))
+    idx, sign = _sum_table(bra.L, aux.l)
+    Rm = R[idx] * pref                                                 # (ntab, ntc, P, Q)
+    X = np.einsum('tsPQ,s,csQ->tcPQ', Rm, sign, aux.Ek, optimize=True)
+    X = X @ aux.seg                                                    # (ntab, nc, P, nshell)
+    return np.einsum('abtP,tcPk->abkc', bra.Eab, X, optimize=True)
+
+
+def eri2c(auxa: AuxShellSet, auxb: AuxShellSet) -> np.ndarray:
+    """(P|Q) over Cartesian components: (nshell_a, nca, nshell_b, ncb)."""
+    p = auxa.p[:, None]
+    q = auxb.p[None, :]
+    alpha = p * q / (p + q)
+    d = auxa.P[:, None, :] - auxb.P[None, :, :]
+    L = auxa.l + auxb.l
+    R = hermite_r(L, alpha, d[..., 0], d[..., 1], d[..., 2])
+    pref = 2.0 * np.pi ** 2.5 / (p * q * np.sqrt(p + q))
+    idx, sign = _sum_table(auxa.l, auxb.l)
+    Rm = R[idx] * pref
+    X = np.einsum('tsPQ,s,csQ->tcPQ', Rm, sign, auxb.Ek, optimize=True) @ auxb.seg   # (nta, ncb, Pprim, kb)
+    Y = np.einsum('atP,tcPk->aPck', auxa.Ek, X, optimize=True)                      # (nca, Pprim, ncb, kb)
+    Y = np.einsum('aPck,Pj->jakc', Y, auxa.seg, optimize=True)
+    return Y

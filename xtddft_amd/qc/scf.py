@@ -49,7 +49,17 @@ class _SCFBase:
         self.e_tot = 0.0
         self.scf_summary = {}
         self.mo_coeff = self.mo_occ = self.mo_energy = None
+        self.with_df = None
         self._built = False
+
+    def density_fit(self, auxbasis=None):
+        """J/K from a 3-index factor instead of the 4-index ERIs (PySCF
+        ``mf.density_fit()``; the reference's DF mean fields, XTDA.py:518-543).
+        ``auxbasis``: {element: shells} or None for the even-tempered default."""
+        from .df import DF
+        self.with_df = DF(self.mol, auxbasis)
+        self._built = False
+        return self
 
     # ----------------------------------------------------------- set-up
     def build(self):
@@ -59,7 +69,9 @@ class _SCFBase:
         self.comps, self.hyb, self.xctype = _xc.parse_xc(self.xc)
         self.s1e = mol.intor("int1e_ovlp")
         self.h1e = mol.intor("int1e_kin") + mol.intor("int1e_nuc")
-        self.eri = mol.eri_full()
+        self.eri = mol.eri_full() if self.with_df is None else None
+        if self.with_df is not None:
+            self.with_df.build()
         if self.xctype != "HF":
             if self.grids is None:
                 self.grids = gen_grids(mol)
@@ -85,11 +97,19 @@ class _SCFBase:
     # -------------------------------------------------------- potentials
     def get_jk(self, mol=None, dm=None, hermi=1, with_j=True, with_k=True):
         """PySCF incore convention: vj = (ij|kl) D_kl, vk = (ij|kl) D_jk -> [i,l]."""
+        if self.with_df is not None:
+            return self.with_df.get_jk(dm, with_j, with_k)
         d = np.asarray(dm, dtype=np.float64)
         shape = d.shape
-        d = d.reshape(-1, shape[-2], shape[-1])
-        vj = np.einsum('ijkl,xkl->xij', self.eri, d).reshape(shape) if with_j else None
-        vk = np.einsum('ijkl,xjk->xil', self.eri, d).reshape(shape) if with_k else None
+        n = shape[-1]
+        d = d.reshape(-1, n * n)
+        eri = self.eri.reshape(n * n, n * n)
+        vj = (eri @ d.T).T.reshape(shape) if with_j else None
+        vk = None
+        if with_k:
+            if getattr(self, "_eri_k", None) is None:
+                self._eri_k = np.ascontiguousarray(self.eri.transpose(0, 3, 1, 2)).reshape(n * n, n * n)
+            vk = (self._eri_k @ d.T).T.reshape(shape)
         return vj, vk
 
     def _rho(self, dm):
@@ -479,8 +499,12 @@ def _meanfield(mf, chol_tol):
     mol = mf.mol
     nao = mol.nao
     dms = mf._dm
-    eri8 = pack_s8(mf.eri)
-    cderi = pivoted_cholesky(mf.eri.reshape(nao * nao, nao * nao), chol_tol).reshape(-1, nao, nao)
+    if mf.with_df is not None:      # DF mean field: the fitted factor, no 4-index ERIs
+        eri8 = None
+        cderi = mf.with_df.cderi
+    else:
+        eri8 = pack_s8(mf.eri)
+        cderi = pivoted_cholesky(mf.eri.reshape(nao * nao, nao * nao), chol_tol).reshape(-1, nao, nao)
     veff_hf = mf.get_veff_hf(dms)
     omega, alpha, hyb = (0.0, 0.0, 1.0) if mf.xctype == "HF" else _xc.rsh_and_hybrid_coeff(mf.xc)
     grids = fxc = fxc_sf = None
