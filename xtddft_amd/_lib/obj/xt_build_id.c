@@ -1,2 +1,2 @@
-static const char id[] = "XT_BUILD_ID:c6b44f5bbeb7630653153089d7bc0238";
+static const char id[] = "XT_BUILD_ID:f024e0402410c51a44e1d0742914800c";
 const char* xt_build_id(void) { return id + 12; }

@@ -76,7 +76,8 @@ __device__ __forceinline__ double rows_sum4(double v) {
 // TAG only gives hot call sites their own kernel symbol (rocprofv3 identity).
 // MINW = waves per SIMD the register budget must allow (occupancy target).
 // MODE: 0 plain GEMM, 1 / 2 fused XC contractions (XcFuse, xt_internal.h).
-template <int BM, int BN, int WGM, int WGN, int BK, int MINW, bool A_KC, bool B_KC, int TAG, int MODE = 0>
+template <int BM, int BN, int WGM, int WGN, int BK, int MINW, bool A_KC, bool B_KC, int TAG, int MODE = 0,
+          int MAP = 0>
 __global__ void __launch_bounds__(64 * WGM * WGN, MINW)
 dgemm_kernel(GemmParams p) {
   static_assert(MODE == 0 || ((BM == 128 || (MODE == 2 && BM == 64)) && WGM * WGN == 8 && !A_KC && B_KC),
@@ -193,12 +194,21 @@ dgemm_kernel(GemmParams p) {
   //  BK 16 x BN 64 (4 xg x 16 a): g2 = tid >> 5, xg_l = tid >> 3 & 3, a_l = 2 (tid & 7) + u:
   //    3 rho + 6 gradient loads for 2 elements; stores of a 16-lane group hit
   //    columns 2 ap + u + {0, 16} (pitch 17: distinct bank pairs).
+  //  MAP 1, BK 16 x BN 64: g2 = tid >> 5, xg_l = 2 (tid >> 4 & 1) + x, a_l = tid & 15: a
+  //    16-lane group covers the 16 a of one xg -- coalesced 128-B gradient loads, one
+  //    broadcast rho load per (xg, c), and LDS stores on 16 distinct bank pairs
+  //    (MAP 0 puts two xg 16 columns apart in one group: 2-way ds_write_b64 conflicts).
   static_assert(MODE != 2 || (BK == 32 && BN == 128 && NTHREADS == 512) ||
                 (BK == 16 && BN == 64 && NTHREADS == 512), "mode 2 staging map");
-  constexpr int NX = BN == 128 ? 2 : 1, NU = BN == 128 ? 4 : 2;
+  static_assert(MAP == 0 || (BK == 16 && BN == 64), "MAP 1 is the BK 16 x BN 64 map");
+  constexpr int NX = BN == 128 ? 2 : (MAP == 1 ? 2 : 1), NU = BN == 128 ? 4 : (MAP == 1 ? 1 : 2);
   const int g2 = BN == 128 ? (tid >> 6) * 4 + ((tid >> 2) & 3) : tid >> 5;
-  auto xg_loc = [&](int x) XT_INLINE { return BN == 128 ? 2 * ((tid >> 4) & 3) + x : (tid >> 3) & 3; };
-  auto a_loc = [&](int u) XT_INLINE { return BN == 128 ? 4 * (tid & 3) + u : 2 * (tid & 7) + u; };
+  auto xg_loc = [&](int x) XT_INLINE {
+    return BN == 128 ? 2 * ((tid >> 4) & 3) + x : (MAP == 1 ? 2 * ((tid >> 4) & 1) + x : (tid >> 3) & 3);
+  };
+  auto a_loc = [&](int u) XT_INLINE {
+    return BN == 128 ? 4 * (tid & 3) + u : (MAP == 1 ? (tid & 15) : 2 * (tid & 7) + u);
+  };
   int xg2[NX], a2[NU];
   bool ok2[NX][NU];
 #pragma unroll
@@ -570,11 +580,20 @@ static const Cfg kCfg[] = {   // (bm, bn, bk, concurrent block slots, wgm, wgn)
   {128, 64, 16, 512, 2, 4},    // 7: 128x64, 8 waves of 64x16, BK 16, two blocks per CU
 };
 
-template <int BM, int BN, int WGM, int WGN, int BKT, int MINW, bool AK, bool BKc, int TAG, int MODE = 0>
+template <int BM, int BN, int WGM, int WGN, int BKT, int MINW, bool AK, bool BKc, int TAG, int MODE = 0,
+          int MAP = 0>
 static void launch_one(const GemmParams& p, hipStream_t st) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, BKT, MINW, AK, BKc, TAG, MODE>),
+  hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, BKT, MINW, AK, BKc, TAG, MODE, MAP>),
                      dim3(tiles, 1, p.nbatch * p.nsplit), dim3(64 * WGM * WGN), 0, st, p);
+}
+
+// Tuning knobs (environment, read once): XT_W_BN=128 runs the fused rho-forward
+// GEMM on 128-point grid tiles (one block per CU); XT_M_MAP=0 restores the old
+// mode-2 staging map.
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
 }
 
 // Tagged call sites get their own kernel symbol for their one operand layout:
@@ -752,12 +771,20 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
     p.ws = ws;
   }
   if (mode == 1) {
-    launch_one<128, 64, 2, 4, 16, 4, false, true, 4, 1>(p, st);
+    static const int w_bn = env_int("XT_W_BN", 64);
+    if (w_bn == 128) launch_one<128, 128, 2, 4, 16, 2, false, true, 4, 1>(p, st);
+    else             launch_one<128, 64, 2, 4, 16, 4, false, true, 4, 1>(p, st);
   } else if (mode == 2) {
     static_assert(XC_M_BN == 64, "mode 2 launch");
+    static const int m_map = env_int("XT_M_MAP", 1);
     // rows = occupied orbitals: a 64-row tile when they fit (small molecules)
-    if (d.M <= 64) launch_one<64, 64, 2, 4, 16, 4, false, true, 5, 2>(p, st);
-    else           launch_one<128, 64, 2, 4, 16, 4, false, true, 5, 2>(p, st);
+    if (m_map == 1) {
+      if (d.M <= 64) launch_one<64, 64, 2, 4, 16, 4, false, true, 5, 2, 1>(p, st);
+      else           launch_one<128, 64, 2, 4, 16, 4, false, true, 5, 2, 1>(p, st);
+    } else {
+      if (d.M <= 64) launch_one<64, 64, 2, 4, 16, 4, false, true, 5, 2>(p, st);
+      else           launch_one<128, 64, 2, 4, 16, 4, false, true, 5, 2>(p, st);
+    }
   } else switch (cfg) {
     case 0: launch_cfg<128, 128, 2, 4, 32, 2>(p, st, akc, bkc, d.tag); break;
     case 1: launch_cfg<128, 128, 2, 2, 16, 2>(p, st, akc, bkc, d.tag); break;
