@@ -1,0 +1,60 @@
+"""GPU: the molecular front end on the device.
+
+The SCF's J/K and XC through the library's GEMM engine with the DF factor and
+the grid in HBM (``qc.device.DeviceEngine``) against the host SCF: energies to
+1e-9 Ha, the cached TDA kernels (fxc, ALDA0 fxc_ab) to round-off; and a
+density-fitted mean field driving the device XSF-TDA to the reference's stored
+roots within the DF error.
+"""
+import numpy as np
+import pytest
+
+from molecules import HF_IRREP_NELEC, hf_mol, reference_outputs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch(hiplib):
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch
+
+
+def _scf(kind, device, df=False, conv=1e-10):
+    from xtddft_amd.qc import ROKS, UKS
+    mf = (ROKS if kind == "ROKS" else UKS)(hf_mol(), "bhandhlyp")
+    mf.irrep_nelec = dict(HF_IRREP_NELEC)
+    mf.conv_tol = conv
+    if df:
+        mf.density_fit()
+    if device:
+        mf.to_device(0)
+    mf.kernel()
+    assert mf.converged
+    return mf
+
+
+@pytest.mark.parametrize("kind", ["ROKS", "UKS"])
+def test_device_scf_equals_host(torch, kind):
+    host, dev = _scf(kind, False), _scf(kind, True)
+    assert dev.device_engine is not None
+    assert abs(dev.e_tot - host.e_tot) < 1e-9
+    assert abs(dev.e_tot - reference_outputs()[f"{kind.lower()}_bhandhlyp_e_tot"]) < 1e-8
+    mh, md = host.to_meanfield(), dev.to_meanfield()
+    assert np.abs(md.fxc - mh.fxc).max() < 1e-10 * np.abs(mh.fxc).max()
+    assert np.abs(md.fxc_sf - mh.fxc_sf).max() < 1e-10 * np.abs(mh.fxc_sf).max()
+
+
+def test_density_fitted_device_scf_and_xsf(torch):
+    """DF mean field built on the device (no 4-index ERIs anywhere) drives the
+    device XSF-TDA; roots within the DF error (~1e-4 Ha) of the reference's."""
+    from molecules import HA2EV_XSF
+    from xtddft_amd.xsf_tda import XSF_TDA
+    host, dev = _scf("ROKS", False, df=True), _scf("ROKS", True, df=True)
+    assert abs(dev.e_tot - host.e_tot) < 1e-9
+    mf = dev.to_meanfield()
+    assert mf.eri is None and mf.jk_mode == "DF"
+    ref = reference_outputs()
+    e, _ = XSF_TDA(mf).kernel(nstates=10, fglobal=ref["xsf_roks_alda0_fglobal"])
+    assert np.abs(np.asarray(e) / HA2EV_XSF - np.asarray(ref["xsf_roks_alda0_ev"]) / HA2EV_XSF).max() < 5e-4

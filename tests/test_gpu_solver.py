@@ -110,3 +110,19 @@ def test_properties_at_larger_size(torch, kind):
     # the batch size does not change a vector's image
     single = op.apply(x[2:3])
     assert np.abs(single - ax[2:3]).max() < 1e-13 * np.abs(single).max()
+
+
+def test_davidson_follow_state_and_lessio_accepted(torch):
+    """follow_state (Davidson.py:246-253) restarts from the previous Ritz vectors
+    only on a residual blow-up; on a regular problem it leaves the roots unchanged.
+    lessio has no effect with the subspace in memory, as in the reference."""
+    from xtddft_amd.davidson import DiagPrecond, davidson1
+    from xtddft_amd.operator import DeviceOperator
+    mf = make_mf(nao=30, nc=6, no=2, xctype="GGA", hyb=0.2)
+    vind, hdiag = oxtda.gen_tda_operation(mf)
+    x0 = oxtda.get_init_guess(mf, 4)
+    op = DeviceOperator(mf, "XTDA")
+    kw = dict(tol_residual=1e-6, lindep=1e-12, nroots=4, pick=oxtda.pickeig, max_cycle=100)
+    c1, e1, _, _ = davidson1(op.apply, x0, DiagPrecond(hdiag, 0.0), **kw)
+    c2, e2, _, _ = davidson1(op.apply, x0, DiagPrecond(hdiag, 0.0), follow_state=True, lessio=True, **kw)
+    assert c1.all() and c2.all() and np.abs(np.asarray(e1) - np.asarray(e2)).max() < 1e-10

@@ -1,2 +1,2 @@
-static const char id[] = "XT_BUILD_ID:f024e0402410c51a44e1d0742914800c";
+static const char id[] = "XT_BUILD_ID:8d13ecbb9d581cf5e109f86b35e71079";
 const char* xt_build_id(void) { return id + 12; }

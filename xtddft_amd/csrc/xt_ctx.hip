@@ -913,9 +913,9 @@ static int xc_response(xt_ctx* c, int nz) {
       RET(gemm(c, b1));
       if (gga) {
         GemmDesc b2;   // accT[i][(xg,a)] += sum_g PhiO0[g][i] sum_c wv_c[g][xg] dPhiV_c[g][a]
-        b2.M = O; b2.N = xc_m_cols(nzg, V); b2.K = n;
+        b2.M = O; b2.N = xc_m_cols(nzg, V, xc_m_bn()); b2.K = n;
         b2.A = PO; b2.sAm = 1; b2.sAk = nmo;
-        b2.fz.mode = 2; b2.fz.V = V; b2.fz.nx = nzg;
+        b2.fz.mode = 2; b2.fz.V = V; b2.fz.nx = nzg; b2.fz.mbn = xc_m_bn();
         b2.fz.w = PV + compP; b2.fz.wc = compP; b2.fz.wg = nmo;
         b2.fz.rho = Rg[q]; b2.fz.rg = ldR[q];
         b2.C = c->accT.p + gr[q].ch0 * chs; b2.ldc = (long)nzg * V; b2.beta = 1.0;

@@ -73,6 +73,29 @@ __device__ __forceinline__ double rows_sum4(double v) {
   return pair32(pair16(v));
 }
 
+// Row-pair swaps (v_permlane32_swap / v_permlane16_swap on both halves of a double):
+// swap32(A, B) exchanges A's lanes 32-63 with B's lanes 0-31; swap16(A, B) A's lanes
+// 16-31 / 48-63 with B's 0-15 / 32-47.  After swap32(A, B); A += B the lower half
+// holds A summed over the two halves and the upper half B's; swap16 then does the
+// same inside each half: a transposing 4-row reduction (each row of lanes ends
+// with the full sum of one of four values).
+__device__ __forceinline__ void swap32_d(double& A, double& B) {
+  const unsigned alo = (unsigned)__double2loint(A), ahi = (unsigned)__double2hiint(A);
+  const unsigned blo = (unsigned)__double2loint(B), bhi = (unsigned)__double2hiint(B);
+  const auto lo = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+  A = __hiloint2double((int)hi[0], (int)lo[0]);
+  B = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void swap16_d(double& A, double& B) {
+  const unsigned alo = (unsigned)__double2loint(A), ahi = (unsigned)__double2hiint(A);
+  const unsigned blo = (unsigned)__double2loint(B), bhi = (unsigned)__double2hiint(B);
+  const auto lo = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+  A = __hiloint2double((int)hi[0], (int)lo[0]);
+  B = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+
 // TAG only gives hot call sites their own kernel symbol (rocprofv3 identity).
 // MINW = waves per SIMD the register budget must allow (occupancy target).
 // MODE: 0 plain GEMM, 1 / 2 fused XC contractions (XcFuse, xt_internal.h).
@@ -422,7 +445,11 @@ dgemm_kernel(GemmParams p) {
       }
     };
     // contract the accumulators with the weights, reduce over the 16 a of each
-    // row sub-tile (4 in-lane, 4 rows of lanes by rows_sum4), clear them
+    // row sub-tile (4 in-lane FMAs, then the 4 rows of lanes), clear them.  Lane row
+    // q owns sub-tiles i = q (mod 4): a transposing reduction (swap32 + swap16 over
+    // the four sub-tiles of a group) leaves row q with the full sum of sub-tile q --
+    // 3 row swaps per (j, c, group of 4) instead of 4 all-row sums.
+    static_assert(TM % 4 == 0, "transposing reduction over groups of 4 sub-tiles");
     auto reduce = [&]() XT_INLINE {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -433,10 +460,17 @@ dgemm_kernel(GemmParams p) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) wz[t] = smem[2 * STAGE + (c * BN + n) * WP + q + 4 * t];
 #pragma unroll
-          for (int i = 0; i < TM; ++i) {
-            const double sv = rows_sum4(acc[i][j][0] * wz[0] + acc[i][j][1] * wz[1] +
-                                        acc[i][j][2] * wz[2] + acc[i][j][3] * wz[3]);
-            if ((i & 3) == q) racc[i >> 2][j][c] += sv;
+          for (int g4 = 0; g4 < TM / 4; ++g4) {
+            double v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const d4 a = acc[4 * g4 + i][j];
+              v[i] = a[0] * wz[0] + a[1] * wz[1] + a[2] * wz[2] + a[3] * wz[3];
+            }
+            swap32_d(v[0], v[2]); v[0] += v[2];
+            swap32_d(v[1], v[3]); v[1] += v[3];
+            swap16_d(v[0], v[1]); v[0] += v[1];
+            racc[g4][j][c] += v[0];
           }
         }
 #pragma unroll
@@ -548,7 +582,7 @@ __global__ void splitk_reduce(GemmParams p) {
     const int m = (int)(e / p.N), n = (int)(e % p.N);
     long cn = n;
     if (p.fz.mode == 2) {   // logical column -> xg V + a (see dgemm_kernel mode 2)
-      const int bn = XC_M_BN, xgb = bn / 16;
+      const int bn = p.fz.mbn, xgb = bn / 16;
       const int nxb = (p.fz.nx + xgb - 1) / xgb, tn = n / bn, cc = n % bn;
       const int xg = (tn % nxb) * xgb + cc / 16, a = (tn / nxb) * 16 + (cc & 15);
       if (xg >= p.fz.nx || a >= p.fz.V) continue;
@@ -594,6 +628,13 @@ static void launch_one(const GemmParams& p, hipStream_t st) {
 static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
+}
+
+// mode 2 tile width: 64 (BK 16, two blocks per CU) or, with XT_M_BN=128, 128 (BK 32,
+// 8 xg x 16 a per column tile, one block per CU)
+int xc_m_bn() {
+  static const int bn = env_int("XT_M_BN", 64) == 128 ? 128 : 64;
+  return bn;
 }
 
 // Tagged call sites get their own kernel symbol for their one operand layout:
@@ -709,8 +750,8 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
   p.nbatch = (d.nb1 > 0 ? d.nb1 : 1) * p.nb2;
   p.ws = nullptr;
   p.fz = d.fz;
-  if (d.fz.mode != 0) {   // fused XC modes: fixed tiles (mode 1 128x64, mode 2 XC_M_BN wide)
-    const Cfg& c = kCfg[7];
+  if (d.fz.mode != 0) {   // fused XC modes: fixed tiles (mode 1 128x64, mode 2 64 / 128 wide)
+    const Cfg& c = (d.fz.mode == 2 && d.fz.mbn == 128) ? kCfg[0] : kCfg[7];
     const long units = (long)p.R * ((d.K + c.bk - 1) / c.bk);
     p.nsplit = d.fz.mode == 1 ? 1 : choose_split(c, d.M, d.N, p.nbatch, units);
     if (d.max_split > 0 && p.nsplit > d.max_split) p.nsplit = d.max_split;
@@ -744,7 +785,8 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
   if (mode != 0 && (d.sAm != 1 || d.fz.w == nullptr || d.fz.rho == nullptr || d.fz.nx <= 0 || d.fz.V <= 0))
     return XT_ERR_ARG;
   if (mode == 1 && (d.sBk != 1 || d.nb1 > 1 || d.nb2 > 1 || d.M != 16 * d.fz.nx)) return XT_ERR_ARG;
-  if (mode == 2 && (d.R > 1 || d.nb1 > 1 || d.nb2 > 1 || d.N != xc_m_cols(d.fz.nx, d.fz.V))) return XT_ERR_ARG;
+  if (mode == 2 && (d.R > 1 || d.nb1 > 1 || d.nb2 > 1 || d.fz.mbn != xc_m_bn() ||
+                    d.N != xc_m_cols(d.fz.nx, d.fz.V, d.fz.mbn))) return XT_ERR_ARG;
   const bool akc = mode == 0 && (d.sAk == 1);
   const bool bkc = mode != 0 || (d.sBk == 1);
   if (!akc && d.sAm != 1) return XT_ERR_ARG;
@@ -775,10 +817,11 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
     if (w_bn == 128) launch_one<128, 128, 2, 4, 16, 2, false, true, 4, 1>(p, st);
     else             launch_one<128, 64, 2, 4, 16, 4, false, true, 4, 1>(p, st);
   } else if (mode == 2) {
-    static_assert(XC_M_BN == 64, "mode 2 launch");
     static const int m_map = env_int("XT_M_MAP", 1);
     // rows = occupied orbitals: a 64-row tile when they fit (small molecules)
-    if (m_map == 1) {
+    if (d.fz.mbn == 128) {
+      launch_one<128, 128, 2, 4, 32, 2, false, true, 5, 2>(p, st);
+    } else if (m_map == 1) {
       if (d.M <= 64) launch_one<64, 64, 2, 4, 16, 4, false, true, 5, 2, 1>(p, st);
       else           launch_one<128, 64, 2, 4, 16, 4, false, true, 5, 2, 1>(p, st);
     } else {

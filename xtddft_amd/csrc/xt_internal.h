@@ -19,10 +19,10 @@ namespace xt {
 //    out: rho[g rg + 3 xg + c] = sum_a W[g, xg, a] w[c wc + g wg + a]   (c < 3)
 //  mode 2 "M backward":   B(g, n) generated as sum_c rho[g rg + 3 xg + c] w[c wc + g wg + a]
 //    with n -> (xg, a) in (XC_M_BN / 16) x 16 blocks (xg-block fastest); C column xg V + a;
-//    N must be xc_m_cols(nx, V).
-constexpr int XC_M_BN = 64;   // mode 2 column-tile width
-inline int xc_m_cols(int nx, int V) {
-  return ((nx + XC_M_BN / 16 - 1) / (XC_M_BN / 16)) * ((V + 15) / 16) * XC_M_BN;
+//    N must be xc_m_cols(nx, V, mbn).
+int xc_m_bn();                // mode 2 column-tile width of the launched variant (64 or 128)
+inline int xc_m_cols(int nx, int V, int bn) {
+  return ((nx + bn / 16 - 1) / (bn / 16)) * ((V + 15) / 16) * bn;
 }
 struct XcFuse {
   int mode = 0;
@@ -32,6 +32,7 @@ struct XcFuse {
   long rg = 0;
   long ablk = 0;               // mode 1: A offset between consecutive xg
   int V = 0, nx = 0;
+  int mbn = 64;                // mode 2: column-tile width (xc_m_bn())
 };
 
 // Public-facing GEMM description (see xt_gemm.hip for the contraction).

@@ -214,6 +214,7 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
     xt = None
     icyc = 0
     x0r = None
+    max_dx_last = 1e9
     for icyc in range(max_cycle):
         if fresh_start:
             space = 0
@@ -259,8 +260,11 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
         vte = torch.as_tensor(np.ascontiguousarray(-(v * e).T), device=dev.device)
         x0r = torch.empty((nr, dim), dtype=torch.float64, device=dev.device)
         dev.gemm(0, 0, nr, dim, space, 1.0, vt, space, xs, dim, 0.0, x0r, dim)     # x0 = v^T xs
+        # ax0 = v^T ax.  (lessio recomputes A x0 only when the subspace is not held
+        # in memory -- lessio = lessio and not _incore, Davidson.py:128; here it
+        # always is, in HBM, so lessio has no effect, as in the reference.)
         r = torch.empty_like(x0r)
-        dev.gemm(0, 0, nr, dim, space, 1.0, vt, space, ax, dim, 0.0, r, dim)       # ax0 = v^T ax
+        dev.gemm(0, 0, nr, dim, space, 1.0, vt, space, ax, dim, 0.0, r, dim)
         dev.gemm(0, 0, nr, dim, space, 1.0, vte, space, xs, dim, 1.0, r, dim)      # r = ax0 - e x0
         dx_norm = np.sqrt(dev.norms2(r).cpu().numpy())
         for k in range(nr):
@@ -269,6 +273,16 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
                   np.abs(de).max())
         if all(conv):
             break
+        max_dx = float(dx_norm.max())
+        if (follow_state and max_dx > 1 and max_dx / max_dx_last > 3 and space > nroots + 2):
+            # large |r|: restart from the previous Ritz vectors (Davidson.py:246-253)
+            log.debug("davidson %d: large |r| %.3g, restoring the previous x0", icyc, max_dx)
+            k = vlast.shape[0]
+            vl = torch.as_tensor(np.ascontiguousarray(vlast.T), device=dev.device)
+            x0 = torch.empty((vlast.shape[1], dim), dtype=torch.float64, device=dev.device)
+            dev.gemm(0, 0, vlast.shape[1], dim, k, 1.0, vl, k, xs, dim, 0.0, x0, dim)
+            fresh_start = True
+            continue
         keep = [k for k in range(nr) if (not conv[k]) and dx_norm[k] ** 2 > lindep]
         if keep:
             rk = r[keep].contiguous()
@@ -293,6 +307,7 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
         if xt.shape[0] == 0:
             conv = dx_norm < toloose
             break
+        max_dx_last = max_dx
         fresh_start = space + nroots > max_space
         if fresh_start:
             x0 = x0r

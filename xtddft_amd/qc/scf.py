@@ -50,7 +50,17 @@ class _SCFBase:
         self.scf_summary = {}
         self.mo_coeff = self.mo_occ = self.mo_energy = None
         self.with_df = None
+        self.device_engine = None
+        self._device = None
         self._built = False
+
+    def to_device(self, device: int = 0):
+        """Evaluate J/K and XC (and the cached TDA kernels) on the GPU through the
+        library's GEMM engine (``qc.device.DeviceEngine``)."""
+        self._device = device
+        self.device_engine = None
+        self._built = False
+        return self
 
     def density_fit(self, auxbasis=None):
         """J/K from a 3-index factor instead of the 4-index ERIs (PySCF
@@ -78,6 +88,9 @@ class _SCFBase:
             self.ao = mol.eval_ao(self.grids.coords, deriv=1 if self.xctype == "GGA" else 0)
             if self.ao.ndim == 2:
                 self.ao = self.ao[None]
+        if self._device is not None:
+            from .device import DeviceEngine
+            self.device_engine = DeviceEngine(self, self._device)
         if mol.symmetry is not None:
             self.ao_irrep = mol.ao_irreps()
         else:
@@ -97,6 +110,8 @@ class _SCFBase:
     # -------------------------------------------------------- potentials
     def get_jk(self, mol=None, dm=None, hermi=1, with_j=True, with_k=True):
         """PySCF incore convention: vj = (ij|kl) D_kl, vk = (ij|kl) D_jk -> [i,l]."""
+        if self.device_engine is not None:
+            return self.device_engine.get_jk(dm, with_j, with_k)
         if self.with_df is not None:
             return self.with_df.get_jk(dm, with_j, with_k)
         d = np.asarray(dm, dtype=np.float64)
@@ -124,6 +139,8 @@ class _SCFBase:
 
     def _vxc(self, dms):
         """(E_xc[DFT], V_xc (2, nao, nao)) at spin densities dms."""
+        if self.device_engine is not None:
+            return self.device_engine.vxc(dms)
         nao = dms.shape[-1]
         vmat = np.zeros((2, nao, nao))
         exc_tot = 0.0
@@ -511,13 +528,16 @@ def _meanfield(mf, chol_tol):
     if mf.xctype != "HF":
         ao = mf.ao
         w = mf.grids.weights
-        rho = np.asarray([mf._rho(dms[0]), mf._rho(dms[1])])
-        fxc = _xc.eval_xc_eff(mf.xc, rho, deriv=2)[2]
-        # ALDA0 (SF_TDA.py:69-85): density-only rho, vxc weighted, divided by rho_a - rho_b + 1e-9
-        rho0 = np.zeros_like(rho)
-        rho0[:, 0] = rho[:, 0]
-        vxc0 = _xc.eval_xc_eff(mf.xc, rho0, deriv=1)[1]
-        fxc_sf = (vxc0[0, 0] * w - vxc0[1, 0] * w) / (rho[0, 0] - rho[1, 0] + 1e-9)
+        if mf.device_engine is not None:
+            fxc, fxc_sf = mf.device_engine.kernels(dms)
+        else:
+            rho = np.asarray([mf._rho(dms[0]), mf._rho(dms[1])])
+            fxc = _xc.eval_xc_eff(mf.xc, rho, deriv=2)[2]
+            # ALDA0 (SF_TDA.py:69-85): density-only rho, vxc weighted, divided by rho_a - rho_b + 1e-9
+            rho0 = np.zeros_like(rho)
+            rho0[:, 0] = rho[:, 0]
+            vxc0 = _xc.eval_xc_eff(mf.xc, rho0, deriv=1)[1]
+            fxc_sf = (vxc0[0, 0] * w - vxc0[1, 0] * w) / (rho[0, 0] - rho[1, 0] + 1e-9)
         grids = Grid(ao=np.ascontiguousarray(ao), weights=np.ascontiguousarray(w))
     mfmol = MFMole(nao=nao, spin=mol.spin, nelectron=mol.nelectron, symmetry=mol.symmetry is not None)
     out = MeanField(mol=mfmol, mo_coeff=mf.mo_coeff, mo_occ=mf.mo_occ, mo_energy=mf.mo_energy,

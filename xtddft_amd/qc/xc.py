@@ -222,3 +222,50 @@ def _eval_xc_eff(torch, xc, rho, deriv):
         H = 0.5 * (H + H.transpose(1, 0, 2))       # exact symmetry (autograd round-off)
         fxc[..., mask] = H.reshape(2, ncomp, 2, ncomp, -1)
     return exc, vxc, fxc
+
+
+def eval_xc_eff_torch(xc: str, rho, deriv: int = 1):
+    """``eval_xc_eff`` on a torch tensor rho (2, ncomp, ngrid) wherever it lives
+    (the device SCF engine evaluates the functional on the GPU): returns torch
+    (exc (ngrid,), vxc (2, ncomp, ngrid), fxc (2, ncomp, 2, ncomp, ngrid) or None)
+    with the same density screening and derivative layout."""
+    import torch
+    comps, _, xctype = parse_xc(xc)
+    ncomp = 4 if xctype == "GGA" else 1
+    if rho.dim() == 2:
+        rho = rho[:, None, :]
+    rho = rho[:, :ncomp].to(torch.float64)
+    ng = rho.shape[-1]
+    kw = dict(dtype=torch.float64, device=rho.device)
+    exc = torch.zeros(ng, **kw)
+    vxc = torch.zeros((2, ncomp, ng), **kw)
+    fxc = torch.zeros((2, ncomp, 2, ncomp, ng), **kw) if deriv >= 2 else None
+    if not comps:
+        return exc, vxc, fxc
+    mask = (rho[0, 0] + rho[1, 0]) > DENS_THRESHOLD
+    idx = torch.nonzero(mask).squeeze(1)
+    if idx.numel() == 0:
+        return exc, vxc, fxc
+    x = rho[:, :, idx].reshape(2 * ncomp, -1).clone().requires_grad_(True)
+    rs = x.reshape(2, ncomp, -1)
+    ra = torch.clamp(rs[0, 0], min=1e-30)
+    rb = torch.clamp(rs[1, 0], min=1e-30)
+    if ncomp == 4:
+        ga, gb = rs[0, 1:], rs[1, 1:]
+        saa, sab, sbb = (ga * ga).sum(0), (ga * gb).sum(0), (gb * gb).sum(0)
+    else:
+        saa = sab = sbb = torch.zeros_like(ra)
+    eps = 0.0
+    for name, coef in comps:
+        eps = eps + coef * _PIECES[name](ra, rb, saa, sab, sbb, torch)
+    g = torch.autograd.grad(eps.sum(), x, create_graph=deriv >= 2)[0]
+    exc[idx] = (eps / (ra + rb)).detach()
+    vxc[:, :, idx] = g.detach().reshape(2, ncomp, -1)
+    if deriv >= 2:
+        n = 2 * ncomp
+        H = torch.empty((n, n, idx.numel()), **kw)
+        for k in range(n):
+            H[k] = torch.autograd.grad(g[k].sum(), x, retain_graph=k < n - 1)[0]
+        H = 0.5 * (H + H.transpose(0, 1))
+        fxc[..., idx] = H.reshape(2, ncomp, 2, ncomp, -1)
+    return exc, vxc, fxc
