@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <utility>
 #include <math.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 #include <string>
@@ -92,6 +93,7 @@ struct xt_ctx {
   // rank partition (xt_set_partition): aux window for J / direct exchange / XSF
   // Delta-A over the resident factor, and the occupied rows of the stored exchange
   int win_p0 = 0, win_np = -1;   // -1: all aux rows
+  bool skinny = true;            // stored exchange through the skinny streaming kernel (XT_SKINNY=0: generic tile)
   int kr0 = 0, kr1 = -1;         // -1: all O rows
 };
 
@@ -113,21 +115,35 @@ static int to_device(xt_ctx* c, DevBuf& dst, const double* src, size_t count, in
   return 0;
 }
 
-static int gemm(xt_ctx* c, const GemmDesc& g) {
-  const bool prof = g.tag > 0 && g.tag < 6 && ((c->prof_mask >> g.tag) & 1);
-  if (prof) {
-    if ((int)c->pev.size() < c->pev_used + 2) {
-      hipEvent_t a, b;
-      HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
-      c->pev.push_back(a); c->pev.push_back(b);
-      c->pev_tag.push_back(0); c->pev_tag.push_back(0);
-    }
-    c->pev_tag[c->pev_used] = g.tag;
-    HIPCHK(hipEventRecord(c->pev[c->pev_used], c->st));
-    c->prof_flops[g.tag] += g.flops > 0 ? g.flops
-                                         : 2.0 * g.M * (double)g.N * g.K * (g.R > 0 ? g.R : 1) *
-                                               (g.nb1 > 0 ? g.nb1 : 1) * (g.nb2 > 0 ? g.nb2 : 1);
+// live timing of a tagged launch class (xt_set_profile): an event pair around it
+static int prof_begin(xt_ctx* c, int tag, double flops, bool* on) {
+  *on = tag > 0 && tag < 6 && ((c->prof_mask >> tag) & 1);
+  if (!*on) return 0;
+  if ((int)c->pev.size() < c->pev_used + 2) {
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a)); HIPCHK(hipEventCreate(&b));
+    c->pev.push_back(a); c->pev.push_back(b);
+    c->pev_tag.push_back(0); c->pev_tag.push_back(0);
   }
+  c->pev_tag[c->pev_used] = tag;
+  HIPCHK(hipEventRecord(c->pev[c->pev_used], c->st));
+  c->prof_flops[tag] += flops;
+  return 0;
+}
+
+static int prof_end(xt_ctx* c, int tag, bool on) {
+  if (!on) return 0;
+  HIPCHK(hipEventRecord(c->pev[c->pev_used + 1], c->st));
+  c->pev_used += 2;
+  c->prof_launches[tag] += 1;
+  return 0;
+}
+
+static int gemm(xt_ctx* c, const GemmDesc& g) {
+  bool prof = false;
+  RET(prof_begin(c, g.tag, g.flops > 0 ? g.flops
+                                       : 2.0 * g.M * (double)g.N * g.K * (g.R > 0 ? g.R : 1) *
+                                             (g.nb1 > 0 ? g.nb1 : 1) * (g.nb2 > 0 ? g.nb2 : 1), &prof));
   size_t need = dgemm_workspace_bytes(g);
   if (need > 0) {
     size_t cap = (size_t)512 << 20;   // 512 MiB split-K workspace cap
@@ -136,12 +152,7 @@ static int gemm(xt_ctx* c, const GemmDesc& g) {
   }
   int r = dgemm(g, c->st, c->ws.p, c->ws.n * sizeof(double));
   if (r) return fail(r, "dgemm launch failed");
-  if (prof) {
-    HIPCHK(hipEventRecord(c->pev[c->pev_used + 1], c->st));
-    c->pev_used += 2;
-    c->prof_launches[g.tag] += 1;
-  }
-  return 0;
+  return prof_end(c, g.tag, prof);
 }
 
 extern "C" {
@@ -208,6 +219,10 @@ int xt_create(const xt_desc* desc, xt_ctx** out) {
     else c->ck_lr = d.alpha - d.hyb;
   }
   for (int i = 0; i < 5; ++i) (void)hipEventCreate(&c->ev[i]);
+  {
+    const char* e = getenv("XT_SKINNY");
+    c->skinny = !(e && atoi(e) == 0);
+  }
   *out = c;
   return 0;
 }
@@ -710,11 +725,17 @@ static int exchange_main(xt_ctx* c, int nz, const DevBuf& B, double coef) {
 // trade when PySCF keeps the ERIs incore (mf._eri, max_memory) rather than
 // running integral-direct J/K.
 // ---------------------------------------------------------------------------
+// row stride of the stored exchange: O V rounded up to 8 doubles (64 B) so every
+// row starts 16-B aligned for the streaming kernel's wide loads
+static size_t kx_ld(const xt_ctx* c) {
+  const size_t ov = (size_t)c->O * c->V;
+  return (ov + 7) & ~(size_t)7;
+}
+
 static size_t kx_doubles(const xt_ctx* c) {
   Group gr[2];
   const int ngr = channel_groups(c, gr);
-  const size_t ov = (size_t)c->O * c->V;
-  return (size_t)(krow1(c) - krow0(c)) * c->V * ov * (size_t)ngr;
+  return (size_t)(krow1(c) - krow0(c)) * c->V * kx_ld(c) * (size_t)ngr;
 }
 
 static bool has_exchange(const xt_ctx* c) {
@@ -754,16 +775,16 @@ static int resolve_kmode(xt_ctx* c) {
 static int build_kx(xt_ctx* c) {
   const int O = c->O, V = c->V, nmo = c->d.nmo, naux = c->d.naux;
   const long mm = (long)nmo * nmo;
-  const size_t ov = (size_t)O * V;
+  const size_t ov = (size_t)O * V, ld = kx_ld(c);
   const int i0 = krow0(c), i1 = krow1(c);
-  const size_t blk = (size_t)(i1 - i0) * V * ov;   // this context's rows of one group
+  const size_t blk = (size_t)(i1 - i0) * V * ld;   // this context's rows of one group
   Group gr[2];
   const int ngr = channel_groups(c, gr);
   if (blk == 0) { c->kx_valid = true; return 0; }
   RET(c->Kx.ensure(blk * ngr));
   HIPCHK(hipMemsetAsync(c->Kx.p, 0, blk * ngr * 8, c->st));
   for (int q = 0; q < ngr; ++q) {
-    double* K = c->Kx.p + (size_t)q * blk - (size_t)i0 * V * ov;   // row (i,a) at (i V + a) ov
+    double* K = c->Kx.p + (size_t)q * blk - (size_t)i0 * V * ld;   // row (i,a) at (i V + a) ld
     for (int pass = 0; pass < 2; ++pass) {
       const double coef = pass ? c->ck_lr : c->ck;
       if (coef == 0.0) continue;
@@ -776,7 +797,7 @@ static int build_kx(xt_ctx* c) {
         g.M = O; g.N = V; g.K = naux; g.nb1 = V;
         g.A = Bo + (long)i * nmo; g.sAm = 1; g.sAk = mm; g.sAb1 = 0;
         g.B = Bv; g.sBk = mm; g.sBn = 1; g.sBb1 = nmo;
-        g.C = K + (size_t)i * V * ov; g.ldc = V; g.sCb1 = (long)ov;
+        g.C = K + (size_t)i * V * ld; g.ldc = V; g.sCb1 = (long)ld;
         g.alpha = coef; g.beta = 1.0;
         RET(gemm(c, g));
       }
@@ -787,20 +808,39 @@ static int build_kx(xt_ctx* c) {
   return 0;
 }
 
+// Per group: acc_g[x][(j,b)] -= sum_{(i,a), i in [i0,i1)} Ze_g[x][(i,a)] Kx_g[(i,a)][(j,b)].
+// Up to SKINNY_MAX_M rows (2 nz <= 48: the headline's 40) the skinny streaming kernel
+// (xt_exch.hip) reads Kx once with wide loads straight into the MFMA operands;
+// more rows take the generic tile, which also reads Kx once.
 static int exchange_stored(xt_ctx* c, int nz) {
-  const size_t ov = (size_t)c->O * c->V;
+  const size_t ov = (size_t)c->O * c->V, ld = kx_ld(c);
   const long chs = (long)nz * ov;
   const int i0 = krow0(c), i1 = krow1(c);
-  const size_t blk = (size_t)(i1 - i0) * c->V * ov;
+  const size_t blk = (size_t)(i1 - i0) * c->V * ld;
   if (blk == 0) return 0;
   Group gr[2];
   const int ngr = channel_groups(c, gr);
   for (int q = 0; q < ngr; ++q) {
-    GemmDesc g;   // acc_g[x][(j,b)] -= sum_{(i,a), i in [i0,i1)} Ze_g[x][(i,a)] Kx_g[(i,a)][(j,b)]
-    g.M = gr[q].nch * nz; g.N = (int)ov; g.K = (i1 - i0) * c->V;
-    g.A = c->ze.p + gr[q].ch0 * chs + (long)i0 * c->V; g.sAm = (long)ov; g.sAk = 1;
-    g.B = c->Kx.p + (size_t)q * blk; g.sBk = (long)ov; g.sBn = 1;
-    g.C = c->acc.p + gr[q].ch0 * chs; g.ldc = (long)ov;
+    const int M = gr[q].nch * nz, K = (i1 - i0) * c->V;
+    const double* A = c->ze.p + gr[q].ch0 * chs + (long)i0 * c->V;
+    const double* B = c->Kx.p + (size_t)q * blk;
+    double* C = c->acc.p + gr[q].ch0 * chs;
+    if (M <= SKINNY_MAX_M && c->skinny) {
+      bool prof = false;
+      RET(prof_begin(c, 1, 2.0 * M * (double)ov * K, &prof));
+      const size_t need = skinny_workspace_bytes(M, (int)ov, K);
+      if (c->ws.n * sizeof(double) < need) RET(c->ws.ensure(need / sizeof(double) + 1));
+      const int r = skinny_gemm(M, (int)ov, K, -1.0, A, (long)ov, B, (long)ld, 1.0, C, (long)ov,
+                                c->ws.p, c->ws.n * sizeof(double), c->st);
+      if (r) return fail(r, "skinny exchange launch failed");
+      RET(prof_end(c, 1, prof));
+      continue;
+    }
+    GemmDesc g;
+    g.M = M; g.N = (int)ov; g.K = K;
+    g.A = A; g.sAm = (long)ov; g.sAk = 1;
+    g.B = B; g.sBk = (long)ld; g.sBn = 1;
+    g.C = C; g.ldc = (long)ov;
     g.alpha = -1.0; g.beta = 1.0;
     g.tag = 1;
     RET(gemm(c, g));

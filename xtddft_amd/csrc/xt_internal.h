@@ -64,6 +64,13 @@ struct GemmParams {
 };
 
 void plan_gemm(const GemmDesc& d, GemmParams* p, int* cfg);
+// skinny streaming GEMM (xt_exch.hip): C = alpha A B + beta C for M <= 48 rows,
+// B (K x N, row stride ldb even, 16-B aligned) streamed once from HBM
+constexpr int SKINNY_MAX_M = 48;
+int skinny_splits(int N, int K);
+size_t skinny_workspace_bytes(int M, int N, int K);
+int skinny_gemm(int M, int N, int K, double alpha, const double* A, long lda, const double* B, long ldb,
+                double beta, double* C, long ldc, double* ws, size_t ws_bytes, hipStream_t st);
 size_t dgemm_workspace_bytes(const GemmDesc& d);
 int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes);
 
