@@ -1,2 +1,2 @@
-static const char id[] = "XT_BUILD_ID:90c8e26bb25cc6f2aa2600046cee66c8";
+static const char id[] = "XT_BUILD_ID:5079571588f33adcf6424e9918988edf";
 const char* xt_build_id(void) { return id + 12; }

@@ -28,6 +28,7 @@
 
 namespace xt {
 
+#define XT_INLINE __attribute__((always_inline))
 typedef double d4x __attribute__((ext_vector_type(4)));
 typedef double d2x __attribute__((ext_vector_type(2)));
 
@@ -50,12 +51,11 @@ k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
   const int k0 = split * kchunk;
   const int k1 = (k0 + kchunk < K) ? k0 + kchunk : K;
   const int nw = strip * SK_BN + wave * (16 * SK_TN);
-  // this lane's 4 physical columns nw + 4 r .. + 3; a lane at the N edge loads its
-  // valid columns one by one (past-N columns read column N - 1 and are not stored)
+  // this lane's 4 physical columns c0 .. c0 + 3.  Rows are readable up to ldb
+  // (a multiple of 4 >= N, zero padding), so a lane with c0 < N loads its 4
+  // columns whole; lanes past N load the last 4 columns and store nothing.
   const int c0 = nw + 4 * r;
-  const bool col_ok = c0 < N;
-  const bool full = c0 + 3 < N;
-  const int nsteps = (k1 - k0 + 3) / 4;          // k-steps of 4
+  const int cl = c0 + 4 <= (int)ldb ? c0 : (int)ldb - 4;
   const int nchunks = (k1 - k0 + SK_BK - 1) / SK_BK;
 
   d4x acc[SK_TM][SK_TN];
@@ -64,95 +64,86 @@ k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
 #pragma unroll
     for (int j = 0; j < SK_TN; ++j) acc[i][j] = (d4x){0.0, 0.0, 0.0, 0.0};
 
-  // A chunk staging: 64 k x 48 m doubles = 1536 16-B pieces, 3 per thread
+  // A chunk staging: 64 k x 48 m doubles = 1536 16-B pieces, 3 per thread; rows
+  // past this split's k1 are zero, which makes whole 16-step chunks safe at the end
   d2x ra[3];
-  auto load_a = [&](int ch) {
+  auto load_a = [&](int ch) XT_INLINE {
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
       const int piece = tid + 512 * e;             // 0..1535
       const int kk = piece / 24, mm = 2 * (piece % 24);
       const int k = k0 + ch * SK_BK + kk;
-      ra[e] = (k < k1) ? *(const d2x*)(AT + (long)k * SK_MP + mm) : (d2x){0.0, 0.0};
+      const d2x v = *(const d2x*)(AT + (long)(k < K ? k : K - 1) * SK_MP + mm);
+      ra[e] = k < k1 ? v : (d2x){0.0, 0.0};
     }
   };
-  auto store_a = [&](int buf) {
+  auto store_a = [&](int buf) XT_INLINE {
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
       const int piece = tid + 512 * e;
       *(d2x*)(&As[buf][(piece / 24) * SK_MP + 2 * (piece % 24)]) = ra[e];
     }
   };
-  // B: k-step s of this split -> row k0 + 4 s + q (clamped to K - 1: rows past
-  // K meet zero A rows)
-  auto load_b = [&](int s, d4x& v) {
-    int k = k0 + 4 * s + q;
-    k = k < K ? k : K - 1;
-    const double* row = B + (long)k * ldb;
-    if (full) {
-      const d2x lo = *(const d2x*)(row + c0), hi = *(const d2x*)(row + c0 + 2);
-      v = (d4x){lo[0], lo[1], hi[0], hi[1]};
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = row[(c0 + j < N) ? c0 + j : N - 1];
-    }
+  // B: k-step s of this split -> row k0 + 4 s + q, clamped to K - 1 (those rows
+  // meet zero A rows); branch-free so the loads pipeline across k-steps
+  auto load_b = [&](int s, d4x& v) XT_INLINE {
+    const int k = k0 + 4 * s + q;
+    const double* p = B + (long)(k < K ? k : K - 1) * ldb + cl;
+    const d2x lo = *(const d2x*)p, hi = *(const d2x*)(p + 2);
+    v = (d4x){lo[0], lo[1], hi[0], hi[1]};
   };
 
   d4x bq[SK_D];
 #pragma unroll
-  for (int t = 0; t < SK_D; ++t) if (t < nsteps) load_b(t, bq[t]);
+  for (int t = 0; t < SK_D; ++t) load_b(t, bq[t]);
   load_a(0);
   store_a(0);
   __syncthreads();
   int s = 0;   // k-step index of this split
   for (int ch = 0; ch < nchunks; ++ch) {
     const int buf = ch & 1;
-    if (ch + 1 < nchunks) load_a(ch + 1);
-    const int steps_here = (nsteps - s < SK_BK / 4) ? nsteps - s : SK_BK / 4;
+    load_a(ch + 1);                                  // (past the last chunk: zeros, unused)
     // 16 k-steps per chunk, unrolled by the ring depth so the ring slots are static
-    for (int t0 = 0; t0 < steps_here; t0 += SK_D) {
+#pragma unroll
+    for (int t0 = 0; t0 < SK_BK / 4; t0 += SK_D) {
 #pragma unroll
       for (int u = 0; u < SK_D; ++u) {
-        if (t0 + u < steps_here) {
-          const int kk = 4 * (t0 + u) + q;           // k within the chunk
-          double af[SK_TM];
+        const int kk = 4 * (t0 + u) + q;             // k within the chunk
+        double af[SK_TM];
 #pragma unroll
-          for (int i = 0; i < SK_TM; ++i) af[i] = As[buf][kk * SK_MP + 16 * i + r];
-          const d4x bv = bq[u];
-          if (s + SK_D < nsteps) load_b(s + SK_D, bq[u]);   // refill this slot
+        for (int i = 0; i < SK_TM; ++i) af[i] = As[buf][kk * SK_MP + 16 * i + r];
+        const d4x bv = bq[u];
+        load_b(s + SK_D, bq[u]);                     // refill this ring slot
 #pragma unroll
-          for (int i = 0; i < SK_TM; ++i)
+        for (int i = 0; i < SK_TM; ++i)
 #pragma unroll
-            for (int j = 0; j < SK_TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bv[j], acc[i][j], 0, 0, 0);
-          ++s;
-        }
+          for (int j = 0; j < SK_TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bv[j], acc[i][j], 0, 0, 0);
+        ++s;
       }
     }
-    if (ch + 1 < nchunks) {
-      // As[buf ^ 1] held chunk ch - 1, read by every wave before the previous
-      // barrier; one barrier publishes chunk ch + 1
-      store_a(buf ^ 1);
-      __syncthreads();
-    }
+    // As[buf ^ 1] held chunk ch - 1, read by every wave before the previous
+    // barrier; one barrier publishes chunk ch + 1
+    store_a(buf ^ 1);
+    __syncthreads();
   }
   // C/D layout: col = lane & 15 (= r), row = 4 reg + q; sub-tile j col r -> 4 r + j
-  if (!col_ok) return;
+  if (c0 >= N) return;
   double* o = out + (long)split * SK_MP * ldo;
 #pragma unroll
   for (int i = 0; i < SK_TM; ++i)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int m = 16 * i + q + 4 * t;
-      const int c = nw + 4 * r;
       d4x v;
 #pragma unroll
       for (int j = 0; j < SK_TN; ++j) v[j] = acc[i][j][t];
-      if (c + 3 < N) {
-        *(d2x*)(o + (long)m * ldo + c) = (d2x){v[0], v[1]};
-        *(d2x*)(o + (long)m * ldo + c + 2) = (d2x){v[2], v[3]};
+      if (c0 + 3 < N) {
+        *(d2x*)(o + (long)m * ldo + c0) = (d2x){v[0], v[1]};
+        *(d2x*)(o + (long)m * ldo + c0 + 2) = (d2x){v[2], v[3]};
       } else {
 #pragma unroll
-        for (int j = 0; j < SK_TN; ++j) if (c + j < N) o[(long)m * ldo + c + j] = v[j];
+        for (int j = 0; j < SK_TN; ++j) if (c0 + j < N) o[(long)m * ldo + c0 + j] = v[j];
       }
     }
 }
@@ -200,7 +191,8 @@ int skinny_gemm(int M, int N, int K, double alpha, const double* A, long lda, co
   if (M <= 0 || N <= 0) return 0;
   if (M > SK_MP || N < 4 || K <= 0) return XT_ERR_ARG;
   if (ws_bytes < skinny_workspace_bytes(M, N, K)) return XT_ERR_ARG;
-  if ((ldb & 1) || (reinterpret_cast<size_t>(B) & 15)) return XT_ERR_ARG;   // 16-B aligned rows
+  // 16-B aligned rows, readable (zero-padded) up to column ldb >= N rounded up to 4
+  if ((ldb & 3) || ldb < ((N + 3) & ~3) || (reinterpret_cast<size_t>(B) & 15)) return XT_ERR_ARG;
   if (K > (1 << 30) / SK_MP) return XT_ERR_ARG;
   const int nsplit = skinny_splits(N, K);
   int kchunk = (K + nsplit - 1) / nsplit;

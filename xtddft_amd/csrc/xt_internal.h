@@ -65,7 +65,8 @@ struct GemmParams {
 
 void plan_gemm(const GemmDesc& d, GemmParams* p, int* cfg);
 // skinny streaming GEMM (xt_exch.hip): C = alpha A B + beta C for M <= 48 rows,
-// B (K x N, row stride ldb even, 16-B aligned) streamed once from HBM
+// B (K x N, 16-B aligned rows of stride ldb: a multiple of 4 >= N, the padding
+// readable) streamed once from HBM
 constexpr int SKINNY_MAX_M = 48;
 int skinny_splits(int N, int K);
 size_t skinny_workspace_bytes(int M, int N, int K);
