@@ -503,8 +503,9 @@ def rank_main(args):
     for _ in range(args.steps):
         step()
         for name, s in op.profile_stats().items():
-            a = stats_acc.setdefault(name, dict(ms=0.0, launches=0, flops=0.0))
+            a = stats_acc.setdefault(name, dict(ms=0.0, launches=0, flops=0.0, bytes=0.0))
             a["ms"] += s["ms"]; a["launches"] += s["launches"]; a["flops"] += s["flops"]
+            a["bytes"] += s.get("bytes", 0.0)
     sync()
     if world > 1:
         dist.barrier()
@@ -518,9 +519,16 @@ def rank_main(args):
     verify = w.verify(z, out) if hasattr(w, "verify") else None   # a workload's own self-check
     phases = op.last_timings()
     roofline = roofline_of(args, stats_acc, args.steps)
-    others = {k: dict(ms_per_step=round(v["ms"] / args.steps, 3),
-                      tflops=round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 3))
-              for k, v in stats_acc.items() if v["launches"]}
+    others = {}
+    for k, v in stats_acc.items():
+        if not v["launches"]:
+            continue
+        comp = v["bytes"] / v["launches"]
+        hbm = load_traffic(args.config, k)
+        others[k] = dict(ms_per_step=round(v["ms"] / args.steps, 3),
+                         tflops=round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 3),
+                         compulsory_bytes_per_launch=comp, hbm_bytes_per_launch=hbm,
+                         traffic_ratio=round(hbm / comp, 3) if hbm and comp > 0 else None)
     workload = (f"{KIND_NAME[args.kind]} A.x, nao={args.nao}, nocc_a/nocc_b={args.nc + args.no}/{args.nc}, "
                 f"dim={op.dim}, nvec={args.nvec}, {args.jk} naux={args.naux}, ngrid={args.ngrid}, "
                 f"xc={args.xc}, hyb={args.hyb}"

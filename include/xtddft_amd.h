@@ -153,6 +153,8 @@ int xt_last_timings(const xt_ctx* ctx, double* out4);
    number of launches, algorithmic flops} */
 int xt_set_profile(xt_ctx* ctx, int tag);
 int xt_profile_stats(const xt_ctx* ctx, int tag, double* out3);
+/* compulsory HBM bytes of class `tag` in the last xt_apply (each operand once) */
+int xt_profile_bytes(const xt_ctx* ctx, int tag, double* bytes);
 
 /* XSF preconditioner J diagonals (XSF_TDA.py:859-913): co_j (nc x no), ov_j (no x nv). */
 int xt_xsf_j_diagonals(xt_ctx* ctx, double* co_j, double* ov_j, int ptr_kind);

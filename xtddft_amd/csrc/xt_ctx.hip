@@ -81,6 +81,7 @@ struct xt_ctx {
   std::vector<int> pev_tag;
   int pev_used = 0;
   double prof_flops[6] = {0, 0, 0, 0, 0, 0};
+  double prof_bytes[6] = {0, 0, 0, 0, 0, 0};   // compulsory HBM bytes (operands once)
   double prof_ms[6] = {0, 0, 0, 0, 0, 0};
   int prof_launches[6] = {0, 0, 0, 0, 0, 0};
   int chol_rank = 0;         // full Cholesky rank of the last xt_set_jk_eri8
@@ -116,7 +117,7 @@ static int to_device(xt_ctx* c, DevBuf& dst, const double* src, size_t count, in
 }
 
 // live timing of a tagged launch class (xt_set_profile): an event pair around it
-static int prof_begin(xt_ctx* c, int tag, double flops, bool* on) {
+static int prof_begin(xt_ctx* c, int tag, double flops, double bytes, bool* on) {
   *on = tag > 0 && tag < 6 && ((c->prof_mask >> tag) & 1);
   if (!*on) return 0;
   if ((int)c->pev.size() < c->pev_used + 2) {
@@ -128,6 +129,7 @@ static int prof_begin(xt_ctx* c, int tag, double flops, bool* on) {
   c->pev_tag[c->pev_used] = tag;
   HIPCHK(hipEventRecord(c->pev[c->pev_used], c->st));
   c->prof_flops[tag] += flops;
+  c->prof_bytes[tag] += bytes;
   return 0;
 }
 
@@ -141,9 +143,12 @@ static int prof_end(xt_ctx* c, int tag, bool on) {
 
 static int gemm(xt_ctx* c, const GemmDesc& g) {
   bool prof = false;
-  RET(prof_begin(c, g.tag, g.flops > 0 ? g.flops
-                                       : 2.0 * g.M * (double)g.N * g.K * (g.R > 0 ? g.R : 1) *
-                                             (g.nb1 > 0 ? g.nb1 : 1) * (g.nb2 > 0 ? g.nb2 : 1), &prof));
+  const double nr = g.R > 0 ? g.R : 1, nb = (double)(g.nb1 > 0 ? g.nb1 : 1) * (g.nb2 > 0 ? g.nb2 : 1);
+  // compulsory bytes: A and B read once, C written once (read too when beta != 0)
+  const double bytes = g.bytes > 0 ? g.bytes
+                                   : 8.0 * nb * (nr * ((double)g.M * g.K + (double)g.K * g.N) +
+                                                 (g.beta != 0.0 ? 2.0 : 1.0) * g.M * (double)g.N);
+  RET(prof_begin(c, g.tag, g.flops > 0 ? g.flops : 2.0 * g.M * (double)g.N * g.K * nr * nb, bytes, &prof));
   size_t need = dgemm_workspace_bytes(g);
   if (need > 0) {
     size_t cap = (size_t)512 << 20;   // 512 MiB split-K workspace cap
@@ -168,6 +173,14 @@ int xt_set_profile(xt_ctx* c, int mask) {
 int xt_profile_stats(const xt_ctx* c, int tag, double* out3) {
   if (!c || !out3 || tag < 1 || tag > 5) return fail(XT_ERR_ARG, "bad argument");
   out3[0] = c->prof_ms[tag]; out3[1] = c->prof_launches[tag]; out3[2] = c->prof_flops[tag];
+  return 0;
+}
+
+// compulsory HBM bytes of GEMM class `tag` in the last xt_apply (every operand
+// read once, the output written once): the denominator of a traffic ratio
+int xt_profile_bytes(const xt_ctx* c, int tag, double* bytes) {
+  if (!c || !bytes || tag < 1 || tag > 5) return fail(XT_ERR_ARG, "bad argument");
+  *bytes = c->prof_bytes[tag];
   return 0;
 }
 
@@ -827,7 +840,7 @@ static int exchange_stored(xt_ctx* c, int nz) {
     double* C = c->acc.p + gr[q].ch0 * chs;
     if (M <= SKINNY_MAX_M && c->skinny) {
       bool prof = false;
-      RET(prof_begin(c, 1, 2.0 * M * (double)ov * K, &prof));
+      RET(prof_begin(c, 1, 2.0 * M * (double)ov * K, 8.0 * ((double)ov * K + (double)M * K + 2.0 * M * (double)ov), &prof));
       const size_t need = skinny_workspace_bytes(M, (int)ov, K);
       if (c->ws.n * sizeof(double) < need) RET(c->ws.ensure(need / sizeof(double) + 1));
       const int r = skinny_gemm(M, (int)ov, K, -1.0, A, (long)ov, B, (long)ld, 1.0, C, (long)ov,
@@ -922,6 +935,8 @@ static int xc_response(xt_ctx* c, int nz) {
         f2.fz.rho = Rg[q]; f2.fz.rg = ldR[q];
         f2.tag = 4;
         f2.flops = 2.0 * nzg * V * (double)n * O;
+        // Zp, PhiO0, dPhiV_{x,y,z} in; rhoW out
+        f2.bytes = 8.0 * ((double)nzg * O * V + (double)n * O + 3.0 * n * V + 3.0 * n * nzg);
         RET(gemm(c, f2));
       }
     }
@@ -961,6 +976,8 @@ static int xc_response(xt_ctx* c, int nz) {
         b2.C = c->accT.p + gr[q].ch0 * chs; b2.ldc = (long)nzg * V; b2.beta = 1.0;
         b2.tag = 5;
         b2.flops = 2.0 * O * (double)nzg * V * n;
+        // PhiO0, dPhiV_{x,y,z}, wv in; accT read + written
+        b2.bytes = 8.0 * ((double)n * O + 3.0 * n * V + 3.0 * n * nzg + 2.0 * O * (double)nzg * V);
         RET(gemm(c, b2));
       }
     }
@@ -1085,7 +1102,7 @@ extern "C" int xt_apply(xt_ctx* c, int nz, const double* z, double* sigma, int p
   RET(c->ze.ensure(nch * chs));
   RET(c->acc.ensure(nch * chs));
   c->pev_used = 0;
-  for (int t = 0; t < 6; ++t) { c->prof_flops[t] = 0.0; c->prof_ms[t] = 0.0; c->prof_launches[t] = 0; }
+  for (int t = 0; t < 6; ++t) { c->prof_flops[t] = 0.0; c->prof_bytes[t] = 0.0; c->prof_ms[t] = 0.0; c->prof_launches[t] = 0; }
   HIPCHK(hipEventRecord(c->ev[0], c->st));
   // ---- embed trial vectors -------------------------------------------------
   if (d.kind == XT_KIND_XTDA || d.kind == XT_KIND_UTDA) embed_xtda(c->st, nz, d.nc, d.no, d.nv, zd, c->ze.p);

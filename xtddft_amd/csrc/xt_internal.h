@@ -49,6 +49,7 @@ struct GemmDesc {
   int max_split = 0;                  // 0 = heuristic
   int tag = 0;                        // kernel identity for profiling (see xt_gemm.hip)
   double flops = 0.0;                 // algorithmic flops for profiling (0: 2 M N K R batch)
+  double bytes = 0.0;                 // compulsory HBM bytes for profiling (0: A, B, C once)
   XcFuse fz;                          // fused XC mode (fz.mode != 0)
 };
 

@@ -269,7 +269,9 @@ class DeviceOperator:
         for tag, name in names.items():
             buf = (ctypes.c_double * 3)()
             _capi.check(self._L.xt_profile_stats(self._h, tag, ctypes.cast(buf, ctypes.c_void_p)), "stats")
-            out[name] = dict(tag=tag, ms=buf[0], launches=int(buf[1]), flops=buf[2])
+            nbytes = ctypes.c_double(0.0)
+            _capi.check(self._L.xt_profile_bytes(self._h, tag, ctypes.byref(nbytes)), "bytes")
+            out[name] = dict(tag=tag, ms=buf[0], launches=int(buf[1]), flops=buf[2], bytes=nbytes.value)
         return out
 
     def xsf_j_diagonals(self):
