@@ -252,7 +252,8 @@ def _oracle_vind(args, mf):
     o.re = bool(args.remove)
     if o.re and o.no > 1:
         o.vects = oxsf.get_vect(o.no)
-    return o.gen_tda_operation_sf(fglobal=0.7 * args.hyb + 0.3)
+    # the preconditioner's J diagonals are solver setup, not A.x: not built here
+    return o.gen_tda_operation_sf(fglobal=0.7 * args.hyb + 0.3, with_hdiag=False)
 
 
 def log(msg):

@@ -143,7 +143,10 @@ class XSFOracle:
                           ov.reshape(ov.shape[0], -1), oo])
 
     # ---------------------------------------------------------------- vind
-    def gen_tda_operation_sf(self, foo=1.0, fglobal=None):
+    def gen_tda_operation_sf(self, foo=1.0, fglobal=None, with_hdiag=True):
+        """with_hdiag=False skips the preconditioner's J diagonals (one J build per
+        64 unit vectors; setup, not part of A.x) and returns the Fock-difference
+        diagonal only -- for timing vind alone (bench.py cpu_baseline)."""
         mf = self.mf
         if fglobal is None:
             fglobal = default_fglobal(mf, method=self.method)
@@ -162,7 +165,13 @@ class XSFOracle:
         fb_oo = fockB[nc:nc + no, nc:nc + no]; fb_ov = fockB[nc:nc + no, nc + no:]
         fb_vo = fockB[nc + no:, nc:nc + no]; fb_vv = fockB[nc + no:, nc + no:]
 
-        hdiag = self.build_preconditioner_hdiag(fglobal)
+        if with_hdiag:
+            hdiag = self.build_preconditioner_hdiag(fglobal)
+        else:
+            fa, fb = mf.fock_mo()
+            hd = fb.diagonal()[self.nocc_b:][None, :] - fa.diagonal()[:self.nocc_a, None]
+            hdiag = np.hstack([hd[:nc, no:].reshape(-1), hd[:nc, :no].reshape(-1),
+                               hd[nc:, no:].reshape(-1), hd[nc:, :no].reshape(-1)])
         if self.re:
             hdiag = self.compress_removed_hdiag(hdiag)
         if self.method == 1:
