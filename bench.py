@@ -103,6 +103,10 @@ def parse(argv=None):
     args = ap.parse_args(argv)
     preset = dict(sa=0, remove=False, jk="DF", ngrid=None)
     preset.update(CONFIGS[args.config])
+    # a shape overridden on the command line is not the profiled preset: its PMC
+    # bytes (roofline.traffic) are unmeasured
+    args.custom = any(getattr(args, k, None) is not None
+                      for k in ("nao", "nc", "no", "naux", "ngrid", "nvec", "hyb", "kind", "sa", "jk"))
     for k, v in preset.items():
         if getattr(args, k, None) is None:
             setattr(args, k, v)
@@ -425,10 +429,11 @@ def load_traffic(config, tag_name):
         return None
 
 
-def roofline_of(args, stats_acc, steps):
+def roofline_of(args, stats_acc, steps, world=1):
     dom_name, dom = max(stats_acc.items(), key=lambda kv: kv[1]["ms"])
     avg_ms = dom["ms"] / max(1, dom["launches"])
-    traffic = load_traffic(args.config, dom_name)
+    # the committed PMC summaries are single-GPU runs of the presets
+    traffic = None if (args.custom or world > 1) else load_traffic(args.config, dom_name)
     if dom_name == "mo_exchange_stored":
         # HBM-bound: streams the stored exchange matrix once per launch (+ Ze in, sigma in/out)
         occ = args.nc if args.kind == "SF_UP" else args.nc + args.no
@@ -519,13 +524,13 @@ def rank_main(args):
     log(f"timed {args.steps} steps: {1e3 * T / args.steps:.2f} ms per step")
     verify = w.verify(z, out) if hasattr(w, "verify") else None   # a workload's own self-check
     phases = op.last_timings()
-    roofline = roofline_of(args, stats_acc, args.steps)
+    roofline = roofline_of(args, stats_acc, args.steps, world)
     others = {}
     for k, v in stats_acc.items():
         if not v["launches"]:
             continue
         comp = v["bytes"] / v["launches"]
-        hbm = load_traffic(args.config, k)
+        hbm = None if (args.custom or world > 1) else load_traffic(args.config, k)
         others[k] = dict(ms_per_step=round(v["ms"] / args.steps, 3),
                          tflops=round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 3),
                          compulsory_bytes_per_launch=comp, hbm_bytes_per_launch=hbm,

@@ -95,6 +95,7 @@ struct xt_ctx {
   // Delta-A over the resident factor, and the occupied rows of the stored exchange
   int win_p0 = 0, win_np = -1;   // -1: all aux rows
   bool skinny = true;            // stored exchange through the skinny streaming kernel (XT_SKINNY=0: generic tile)
+  bool m_kernel = true;          // XC M-backward through xt_xcm.hip (XT_M_KERNEL=0: the engine's mode 2)
   int kr0 = 0, kr1 = -1;         // -1: all O rows
 };
 
@@ -235,6 +236,8 @@ int xt_create(const xt_desc* desc, xt_ctx** out) {
   {
     const char* e = getenv("XT_SKINNY");
     c->skinny = !(e && atoi(e) == 0);
+    const char* em = getenv("XT_M_KERNEL");
+    c->m_kernel = !(em && atoi(em) == 0);
   }
   *out = c;
   return 0;
@@ -483,7 +486,10 @@ int xt_set_grid(xt_ctx* c, const double* ao, const double* w, const double* kern
   const bool sf = (c->d.kind == XT_KIND_SF_DOWN || c->d.kind == XT_KIND_SF_UP || c->d.kind == XT_KIND_XSF);
   // input ao carries ncomp_in components (4 for GGA even on the SF path, which only uses ao[0])
   const int ncomp = c->ncomp;
-  RET(c->Phi.ensure((size_t)c->nbasis * ncomp * ng * nmo));
+  // + zeroed slack rows after the last plane (fused XC kernels read whole K-tiles)
+  const size_t phi_used = (size_t)c->nbasis * ncomp * ng * nmo;
+  RET(c->Phi.ensure(phi_used + (size_t)XC_GRID_SLACK * nmo));
+  HIPCHK(hipMemsetAsync(c->Phi.p + phi_used, 0, (c->Phi.n - phi_used) * sizeof(double), c->st));
   const size_t gchunk_max = ((size_t)1 << 30) / (8 * (size_t)nao);
   const int gc = (int)(gchunk_max < (size_t)ng ? gchunk_max : ng);
   if (ptr_kind == XT_PTR_HOST) RET(c->stage.ensure((size_t)gc * nao));
@@ -905,7 +911,7 @@ static int xc_response(xt_ctx* c, int nz) {
   if (G > (size_t)ng) G = ng;
   if (G < 64) G = 64 < (size_t)ng ? 64 : ng;
   RET(c->ubuf.ensure((size_t)nch * nz * O * G));
-  if (gga) RET(c->wbuf.ensure((size_t)nch * nz * 3 * G));
+  if (gga) RET(c->wbuf.ensure((size_t)nch * nz * 3 * (G + XC_GRID_SLACK)));
   const long compP = (long)ng * nmo;
   const long basP = (long)nc * compP;
   const int nab = (V + 15) / 16;
@@ -967,6 +973,20 @@ static int xc_response(xt_ctx* c, int nz) {
       b1.tag = 3;
       RET(gemm(c, b1));
       if (gga) {
+        if (O <= 128 && c->m_kernel) {
+          // dedicated kernel (xt_xcm.hip); tag 5 timing around it and its reduce
+          bool prof = false;
+          RET(prof_begin(c, 5, 2.0 * O * (double)nzg * V * n,
+                         8.0 * ((double)n * O + 3.0 * n * V + 3.0 * n * nzg + 2.0 * O * (double)nzg * V), &prof));
+          const size_t need = xc_back_m_workspace_bytes(O, nzg, V, n);
+          if (c->ws.n * sizeof(double) < need) RET(c->ws.ensure(need / sizeof(double) + 1));
+          const int r = xc_back_m(O, nzg, V, n, PO, nmo, PV + compP, compP, nmo, Rg[q], ldR[q],
+                                  c->accT.p + gr[q].ch0 * chs, (long)nzg * V, c->ws.p, c->ws.n * sizeof(double),
+                                  c->st);
+          if (r) return fail(r, "xc_back_m launch failed");
+          RET(prof_end(c, 5, prof));
+          continue;
+        }
         GemmDesc b2;   // accT[i][(xg,a)] += sum_g PhiO0[g][i] sum_c wv_c[g][xg] dPhiV_c[g][a]
         b2.M = O; b2.N = xc_m_cols(nzg, V, xc_m_bn()); b2.K = n;
         b2.A = PO; b2.sAm = 1; b2.sAk = nmo;

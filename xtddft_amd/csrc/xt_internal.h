@@ -73,6 +73,14 @@ int skinny_splits(int N, int K);
 size_t skinny_workspace_bytes(int M, int N, int K);
 int skinny_gemm(int M, int N, int K, double alpha, const double* A, long lda, const double* B, long ldb,
                 double beta, double* C, long ldc, double* ws, size_t ws_bytes, hipStream_t st);
+// dedicated XC M-backward (xt_xcm.hip): accT[i][xg V + a] += sum_g PhiO[g][i] *
+// sum_c wv[g][xg][c] dPhiV_c[g][a], O <= 128; split over g through a workspace
+// the grid arrays it reads (PhiO, dPhiV, wv) must stay readable XC_GRID_SLACK rows past
+// the chunk's last point (finite, zero-filled slack after the last grid point)
+constexpr int XC_GRID_SLACK = 64;
+size_t xc_back_m_workspace_bytes(int O, int nx, int V, int n);
+int xc_back_m(int O, int nx, int V, int n, const double* PO, long ldp, const double* W, long wc, long wg,
+              const double* R, long rg, double* C, long ldc, double* ws, size_t ws_bytes, hipStream_t st);
 size_t dgemm_workspace_bytes(const GemmDesc& d);
 int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes);
 

@@ -1,0 +1,329 @@
+// XC M-backward as a dedicated kernel (the GGA half of nr_uks_fxc's projection,
+// XTDA.py:514 through PySCF numint):
+//
+//   accT[i][xg V + a] += sum_g PhiO[g][i] * sum_c wv[g][xg][c] * dPhiV_c[g][a]
+//
+// i < O occupied MO, xg < nx (spin channel, trial vector) pairs, a < V virtual MO,
+// g a grid point of the chunk.  The generated operand M[g][xg][a] = sum_c wv dPhiV
+// (nx V values per grid point) never exists in HBM.
+//
+// Why a kernel of its own (the generic engine's mode 2 runs a 128 x 64 tile, BK 16,
+// two blocks per CU): there each wave does 16 MFMAs between barriers and builds its
+// share of the generated tile into LDS before the barrier, so barrier, staging and
+// generation are a large fraction of the loop.  Here:
+//   * one 8-wave block per CU, wave w owns trial pair xg0 + w and 32 virtuals: a
+//     (16 TM) x 32 accumulator tile, TM = ceil(O / 16) <= 8 row sub-tiles;
+//   * per K-tile of 32 grid points every wave issues 8 k-steps x 2 TM MFMAs
+//     (TM 7: 112, ~7k cycles of matrix pipe) per barrier;
+//   * only RAW inputs are staged through LDS (PhiO tile, the block's 32 columns of
+//     the three gradient planes, the block's 8 x 3 wv values per point); each wave
+//     generates its own B fragments in registers from them (3 FMAs per fragment
+//     element, LDS reads broadcast where 16 lanes share a value);
+//   * LDS images are XOR-swizzled at 16-double granularity on the grid row parity so
+//     the two 16-lane row halves of a 32-lane ds_read_b64 group hit disjoint bank
+//     halves (64 banks x 4 B, MI355X_MICROARCH.md LDS table) and stores of 16
+//     contiguous lanes stay contiguous.
+// Split over the grid (K) for occupancy: each split writes its own slab, reduced in a
+// fixed order (deterministic) and added to accT.
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include "xt_internal.h"
+
+namespace xt {
+
+#define XT_INLINE __attribute__((always_inline))
+typedef double d4m __attribute__((ext_vector_type(4)));
+
+constexpr int BM_BK = 32;        // grid points per K-tile
+constexpr int BM_AB = 32;        // virtuals per block (2 MFMA column sub-tiles per wave)
+constexpr int BM_XB = 8;         // trial pairs per block (one per wave)
+
+// LDS images (doubles), one buffer:
+//   A  [g 32][i 16 TM]        swizzle i ^ 16 (g & 1) for even TM (odd TM: the row pitch
+//                             16 TM = 16 mod 32 doubles already separates the halves)
+//   W  [c 3][g 32][a 32]      swizzle a ^ 16 (g & 1)
+//   R  [g 32][xg 8][c 3]      (broadcast reads)
+template <int TM>
+struct BmLds {
+  static constexpr int A = BM_BK * 16 * TM;
+  static constexpr int W = 3 * BM_BK * BM_AB;
+  static constexpr int R = BM_BK * BM_XB * 3;
+  static constexpr int BUF = A + W + R;
+};
+
+template <int TM, bool GEN_FIRST>
+__global__ void __launch_bounds__(512, 1)
+k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
+            const double* __restrict__ PO, long ldp,
+            const double* __restrict__ Wg, long wc, long wg,
+            const double* __restrict__ R, long rg,
+            double* __restrict__ out, long ldo, long slab) {
+  using L = BmLds<TM>;
+  constexpr int PA = 16 * TM;                  // A row length (i)
+  constexpr int A_LD = BM_BK * PA / 512;       // = TM doubles per thread
+  constexpr int W_LD = 3 * BM_BK * BM_AB / 512;  // = 6
+  constexpr int SWA = TM % 2 == 0 ? 16 : 0;    // A-image swizzle (see BmLds)
+  __shared__ __attribute__((aligned(16))) double sm[2 * L::BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4, r16 = lane & 15;
+
+  // ---- block -> (split, a-tile, xg-tile) -----------------------------------
+  // blocks are dealt round-robin over the 8 XCDs: renumber so each XCD runs a
+  // contiguous range, ordered split-major, then a-tile, xg-tile fastest -- the
+  // xg-tiles sharing one a-tile's gradient columns run side by side on one XCD
+  // (its L2 serves the re-reads) and every block of a split reads the same PhiO rows.
+  const int ntx = (nx + BM_XB - 1) / BM_XB, nta = (V + BM_AB - 1) / BM_AB;
+  const int nblk = gridDim.x;
+  int lid = blockIdx.x;
+  {
+    const int xcd = lid & 7, idx = lid >> 3, qn = nblk >> 3, rem = nblk & 7;
+    lid = xcd * qn + (xcd < rem ? xcd : rem) + idx;
+  }
+  const int xt = lid % ntx;
+  const int at = (lid / ntx) % nta;
+  const int split = lid / (ntx * nta);
+  const int x0 = xt * BM_XB, a0 = at * BM_AB;
+  const int nkt = (n + BM_BK - 1) / BM_BK;
+  const int kt0 = split * ktiles_per_split;
+  const int kt1 = min(kt0 + ktiles_per_split, nkt);
+  const int xg = x0 + wave;                    // this wave's trial pair
+  const bool wave_on = xg < nx;
+
+  // ---- staging maps (per thread, fixed) -------------------------------------
+  // A: element e -> (g = (tid + 512 e) / PA, i = (tid + 512 e) % PA): 16-lane runs of
+  //    consecutive i (one 128-B global segment, one conflict-free ds_write_b64 group)
+  // W: element e -> (c, g, a) with a fastest over 32
+  // R: element e -> (g, xg_l, c), 768 values, threads 0..255 load a second one
+  double ra[A_LD], rw[W_LD], rr[2];
+  // per-thread byte offsets from the K-tile's (wave-uniform) row bases, columns
+  // clamped once here.  Rows past n of the last K-tile are read unclamped: the
+  // callers keep BM_BK rows of zeroed slack after the grid arrays (XC_GRID_SLACK),
+  // and those rows' wv are stored as zero, so they add nothing.
+  unsigned oa[A_LD], ow[W_LD], orr[2];
+#pragma unroll
+  for (int e = 0; e < A_LD; ++e) {
+    const int p = tid + 512 * e, gl = p / PA, i = p % PA;
+    oa[e] = (unsigned)(((long)gl * ldp + min(i, O - 1)) * 8);
+  }
+#pragma unroll
+  for (int e = 0; e < W_LD; ++e) {
+    const int p = tid + 512 * e, gl = (p / BM_AB) % BM_BK, al = p % BM_AB;
+    ow[e] = (unsigned)(((long)gl * wg + min(a0 + al, V - 1)) * 8);
+  }
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int p = min(tid + 512 * e, L::R - 1), gl = p / (3 * BM_XB), xc = p % (3 * BM_XB);
+    orr[e] = (unsigned)(((long)gl * rg + 3 * min(x0 + xc / 3, nx - 1) + xc % 3) * 8);
+  }
+  auto ld8 = [](const double* base, unsigned off) XT_INLINE {
+    return *(const double*)((const char*)base + off);
+  };
+  auto load = [&](int kt) XT_INLINE {
+    const int g0 = kt * BM_BK;
+    const double* pa = PO + (long)g0 * ldp;
+    const double* pr = R + (long)g0 * rg;
+#pragma unroll
+    for (int e = 0; e < A_LD; ++e) ra[e] = ld8(pa, oa[e]);
+#pragma unroll
+    for (int e = 0; e < W_LD; ++e) rw[e] = ld8(Wg + (e / 2) * wc + (long)g0 * wg, ow[e]);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) rr[e] = ld8(pr, orr[e]);
+  };
+  // zeros make the padding inert: grid points past n (R = 0 -> B = 0), virtuals
+  // past V and pairs past nx (their columns are never stored; zero keeps them finite)
+  auto store = [&](int buf, int kt) XT_INLINE {
+    double* s = sm + buf * L::BUF;
+    const int g0 = kt * BM_BK;
+#pragma unroll
+    for (int e = 0; e < A_LD; ++e) {
+      const int p = tid + 512 * e, gl = p / PA, i = p % PA;
+      s[gl * PA + (i ^ ((gl & 1) * SWA))] = ra[e];
+    }
+#pragma unroll
+    for (int e = 0; e < W_LD; ++e) {
+      const int p = tid + 512 * e, c = p / (BM_BK * BM_AB), gl = (p / BM_AB) % BM_BK, al = p % BM_AB;
+      s[L::A + (c * BM_BK + gl) * BM_AB + (al ^ ((gl & 1) << 4))] = a0 + al < V ? rw[e] : 0.0;
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int p = tid + 512 * e;
+      if (p < L::R) {
+        const int gl = p / (3 * BM_XB), xc = p % (3 * BM_XB);
+        s[L::A + L::W + p] = (g0 + gl < n && x0 + xc / 3 < nx) ? rr[e] : 0.0;
+      }
+    }
+  };
+
+  d4m acc[TM][2];
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[t][j] = (d4m){0.0, 0.0, 0.0, 0.0};
+
+  // one K-tile: 8 k-steps; lane (q, r16) feeds k = g_l = 4 s + q.  Row parity of g_l
+  // is the parity of q, so the swizzles are per-lane constants and every LDS address
+  // below is a lane base plus a compile-time offset.
+  // The B fragments of k-step s + 1 are generated before the MFMAs of step s in
+  // program order (their LDS reads and the 3-deep FP64 chain then overlap step s's
+  // matrix work instead of stalling step s + 1's first MFMA); GEN_FIRST instead
+  // builds all 8 steps' fragments up front.
+  const int swl = (q & 1) << 4;
+  const int a_lane = q * PA + ((r16) ^ ((q & 1) * SWA));        // A: row q, column r16 (+16 t via XOR-free add)
+  const int w_lane = L::A + q * BM_AB;                           // W: row q
+  const int r_lane = L::A + L::W + q * (3 * BM_XB) + 3 * wave;   // R: row q, this wave's pair
+  auto compute = [&](int buf) XT_INLINE {
+    const double* s = sm + buf * L::BUF;
+    auto gen = [&](int ks, double* b) XT_INLINE {
+      const double* rrow = s + r_lane + 4 * ks * (3 * BM_XB);
+      const double w0 = rrow[0], w1 = rrow[1], w2 = rrow[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const double* wr = s + w_lane + 4 * ks * BM_AB + ((16 * j + r16) ^ swl);
+        b[j] = w0 * wr[0] + w1 * wr[BM_BK * BM_AB] + w2 * wr[2 * BM_BK * BM_AB];
+      }
+    };
+    auto mma = [&](int ks, const double* b) XT_INLINE {
+      double af[TM];
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        // (16 t + r16) ^ sw = 16 (t ^ (sw / 16)) + r16: the swizzle permutes whole sub-tiles
+        const int tt = SWA ? (t ^ (q & 1)) : t;
+        af[t] = s[q * PA + 4 * ks * PA + 16 * tt + r16];
+      }
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t], b[j], acc[t][j], 0, 0, 0);
+    };
+    if constexpr (GEN_FIRST) {
+      double b[BM_BK / 4][2];
+#pragma unroll
+      for (int ks = 0; ks < BM_BK / 4; ++ks) gen(ks, b[ks]);
+#pragma unroll
+      for (int ks = 0; ks < BM_BK / 4; ++ks) mma(ks, b[ks]);
+    } else {
+      double b[2][2];
+      gen(0, b[0]);
+#pragma unroll
+      for (int ks = 0; ks < BM_BK / 4; ++ks) {
+        if (ks + 1 < BM_BK / 4) gen(ks + 1, b[(ks + 1) & 1]);
+        mma(ks, b[ks & 1]);
+      }
+    }
+  };
+  (void)a_lane;
+
+  if (kt0 < kt1) {
+    load(kt0);
+    store(0, kt0);
+    __syncthreads();
+    int buf = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = kt + 1 < kt1;
+      if (more) load(kt + 1);
+      if (wave_on) compute(buf);
+      // the LDS stores (and their vmcnt waits) stay behind every MFMA of this tile
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) store(buf ^ 1, kt + 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+  if (!wave_on) return;
+  // C/D layout: col = lane & 15, row = q + 4 reg
+  double* o = out + (long)split * slab;
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 16 * t + q + 4 * r;
+      if (i >= O) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int a = a0 + 16 * j + r16;
+        if (a < V) o[(long)i * ldo + (long)xg * V + a] = acc[t][j][r];
+      }
+    }
+}
+
+// accT[i][col] += sum_s ws[s][i][col]   (fixed order)
+__global__ void k_xc_back_m_reduce(int O, long cols, int nsplit, const double* __restrict__ ws, long slab,
+                                   double* __restrict__ C, long ldc) {
+  const long total = (long)O * cols;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const long i = t / cols, col = t % cols;
+    double s = 0.0;
+    for (int sp = 0; sp < nsplit; ++sp) s += ws[sp * slab + i * cols + col];
+    C[i * ldc + col] += s;
+  }
+}
+
+// Split count: the fewest splits whose blocks fill the chip's 256 CUs in whole rounds
+// (within 3 %) while keeping >= 16 K-tiles per split.
+static int back_m_splits(int tiles, int nkt) {
+  int best = 1;
+  double best_eff = 0.0;
+  for (int s = 1; s <= 64; ++s) {
+    if (s > 1 && nkt / s < 16) break;
+    const long blocks = (long)tiles * s;
+    const double rounds = (double)blocks / 256.0;
+    const double eff = rounds / ((blocks + 255) / 256);
+    if (eff > best_eff + 0.03 || (best_eff < 0.97 && eff > best_eff)) { best_eff = eff; best = s; }
+    if (eff >= 0.97 && blocks >= 512) break;
+  }
+  return best;
+}
+
+size_t xc_back_m_workspace_bytes(int O, int nx, int V, int n) {
+  const int tiles = ((nx + BM_XB - 1) / BM_XB) * ((V + BM_AB - 1) / BM_AB);
+  const int s = back_m_splits(tiles, (n + BM_BK - 1) / BM_BK);
+  return sizeof(double) * (size_t)s * O * (size_t)nx * V;
+}
+
+template <int TM>
+static void launch_back_m(int O, int nx, int V, int n, int kps, int blocks, const double* PO, long ldp,
+                          const double* W, long wc, long wg, const double* R, long rg, double* ws, long slab,
+                          hipStream_t st) {
+  static const int gen_first = [] { const char* e = getenv("XT_M_GEN"); return e ? atoi(e) : 0; }();
+  if (gen_first)
+    hipLaunchKernelGGL((k_xc_back_m<TM, true>), dim3(blocks), dim3(512), 0, st, O, nx, V, n, kps, PO, ldp, W, wc, wg,
+                       R, rg, ws, (long)nx * V, slab);
+  else
+    hipLaunchKernelGGL((k_xc_back_m<TM, false>), dim3(blocks), dim3(512), 0, st, O, nx, V, n, kps, PO, ldp, W, wc, wg,
+                     R, rg, ws, (long)nx * V, slab);
+}
+
+int xc_back_m(int O, int nx, int V, int n, const double* PO, long ldp, const double* W, long wc, long wg,
+              const double* R, long rg, double* C, long ldc, double* ws, size_t ws_bytes, hipStream_t st) {
+  if (O <= 0 || nx <= 0 || V <= 0 || n <= 0) return 0;
+  if (O > 128) return XT_ERR_ARG;                      // one row tile (the engine's mode 2 covers more)
+  const int tiles = ((nx + BM_XB - 1) / BM_XB) * ((V + BM_AB - 1) / BM_AB);
+  const int nkt = (n + BM_BK - 1) / BM_BK;
+  const int s = back_m_splits(tiles, nkt);
+  const long slab = (long)O * nx * V;
+  if (ws_bytes < sizeof(double) * (size_t)s * slab) return XT_ERR_ARG;
+  const int kps = (nkt + s - 1) / s;
+  const int used = (nkt + kps - 1) / kps;              // splits that own K-tiles
+  const int blocks = tiles * used;
+  const int TM = (O + 15) / 16;
+  switch (TM) {
+    case 1: launch_back_m<1>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+    case 2: launch_back_m<2>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+    case 3: launch_back_m<3>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+    case 4: launch_back_m<4>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+    case 5: launch_back_m<5>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+    case 6: launch_back_m<6>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+    case 7: launch_back_m<7>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+    default: launch_back_m<8>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+  }
+  const long total = slab;
+  int rb = (int)((total + 255) / 256);
+  if (rb > 8192) rb = 8192;
+  hipLaunchKernelGGL(k_xc_back_m_reduce, dim3(rb), dim3(256), 0, st, O, (long)nx * V, used, ws, slab, C, ldc);
+  return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
+}
+
+}  // namespace xt
