@@ -96,6 +96,8 @@ struct xt_ctx {
   int win_p0 = 0, win_np = -1;   // -1: all aux rows
   bool skinny = true;            // stored exchange through the skinny streaming kernel (XT_SKINNY=0: generic tile)
   bool m_kernel = true;          // XC M-backward through xt_xcm.hip (XT_M_KERNEL=0: the engine's mode 2)
+  bool w_kernel = true;          // XC rho-forward through xt_xcw.hip (XT_W_KERNEL=0: the engine's mode 1)
+  bool xsf_fused = true;         // XSF Delta-A exchange through the stored matrix (XT_XSF_FUSED=0: direct)
   int kr0 = 0, kr1 = -1;         // -1: all O rows
 };
 
@@ -238,6 +240,10 @@ int xt_create(const xt_desc* desc, xt_ctx** out) {
     c->skinny = !(e && atoi(e) == 0);
     const char* em = getenv("XT_M_KERNEL");
     c->m_kernel = !(em && atoi(em) == 0);
+    const char* ew = getenv("XT_W_KERNEL");
+    c->w_kernel = !(ew && atoi(ew) == 0);
+    const char* ex = getenv("XT_XSF_FUSED");
+    c->xsf_fused = !(ex && atoi(ex) == 0);
   }
   *out = c;
   return 0;
@@ -867,6 +873,62 @@ static int exchange_stored(xt_ctx* c, int nz) {
   return 0;
 }
 
+// XSF with spin adaptation SA >= 2 through the stored matrix: the main exchange
+// (-Kx z) and the twelve Delta-A exchange projections (XSF_TDA.py:1175-1274, the
+// direct sandwiches of xsf_delta_a) are all sub-blocks of Kx applied to the four
+// source blocks of z, so ONE stream of Kx with the four blocks as 4 nz rows gives
+// every term; a 4 x 4 weight table (source block, target block) combines them.
+// Kx carries c_K: the Delta-A coefficients (on sum_P B B) are divided by it.
+static bool xsf_fused_k(const xt_ctx* c) {
+  const xt_desc& d = c->d;
+  return d.kind == XT_KIND_XSF && d.sa > 1 && c->k_resolved == 1 && c->ck != 0.0 && c->ck_lr == 0.0 &&
+         c->nchan == 1 && c->xsf_fused;
+}
+
+static int exchange_stored_xsf(xt_ctx* c, int nz) {
+  const xt_desc& d = c->d;
+  const int O = c->O, V = c->V, nc = d.nc, no = d.no;
+  const size_t ov = (size_t)O * V, ld = kx_ld(c);
+  const int i0 = krow0(c), i1 = krow1(c);
+  const size_t blk = (size_t)(i1 - i0) * V * ld;
+  if (blk == 0) return 0;
+  const int K = (i1 - i0) * V;
+  const int zmax = SKINNY_MAX_M / 4;           // trial vectors per Kx stream
+  // coefficient table (xsf_delta_a's sandwich coefficients / c_K), source X -> target Y
+  const double si = no / 2.0, fg = d.fglobal, ff = fg * d.foo, tsm1 = 2 * si - 1;
+  const double f1 = sqrt((2 * si + 1) / (2 * si)) - 1;
+  const double f2 = sqrt((2 * si + 1) / (2 * si - 1));
+  const double f3 = sqrt((2 * si) / (2 * si - 1)) - 1;
+  enum { CV = 0, CO = 1, OV = 2, OO = 3 };
+  double dk[4][4] = {};
+  dk[CO][CV] = dk[CV][CO] = dk[OV][CV] = dk[CV][OV] = -fg * f1;   // cv_co, co_cv, cv_ov, ov_cv
+  dk[OV][CO] = dk[CO][OV] = -fg / tsm1;                           // co_ov, ov_co
+  if (d.sa > 2) {
+    dk[OO][CV] = dk[CV][OO] = -ff * (f2 - 1);                     // cv_oo, oo_cv
+    dk[OO][CO] = dk[CO][OO] = dk[OO][OV] = dk[OV][OO] = -ff * f3; // co_oo, oo_co, ov_oo, oo_ov
+  }
+  W16 w;
+  for (int X = 0; X < 4; ++X)
+    for (int Y = 0; Y < 4; ++Y) w.w[4 * X + Y] = -1.0 + dk[X][Y] / c->ck;   // main exchange: -Kx z
+  for (int z0 = 0; z0 < nz; z0 += zmax) {
+    const int nzb = nz - z0 < zmax ? nz - z0 : zmax, M = 4 * nzb;
+    RET(c->zr.ensure((size_t)M * ov));
+    RET(c->tbuf.ensure((size_t)M * ov));
+    xsf_split4(c->st, nzb, O, V, nc, no, c->ze.p + (size_t)z0 * ov, c->zr.p);
+    bool prof = false;
+    RET(prof_begin(c, 1, 2.0 * M * (double)ov * K, 8.0 * ((double)ov * K + (double)M * K + 2.0 * M * (double)ov),
+                   &prof));
+    const size_t need = skinny_workspace_bytes(M, (int)ov, K);
+    if (c->ws.n * sizeof(double) < need) RET(c->ws.ensure(need / sizeof(double) + 1));
+    const int r = skinny_gemm(M, (int)ov, K, 1.0, c->zr.p + (long)i0 * V, (long)ov, c->Kx.p, (long)ld, 0.0,
+                              c->tbuf.p, (long)ov, c->ws.p, c->ws.n * sizeof(double), c->st);
+    if (r) return fail(r, "skinny exchange launch failed");
+    RET(prof_end(c, 1, prof));
+    xsf_combine4(c->st, nzb, O, V, nc, no, w, c->tbuf.p, c->acc.p + (size_t)z0 * ov);
+  }
+  return 0;
+}
+
 extern "C" int xt_set_exchange_mode(xt_ctx* c, int mode, double max_gib) {
   if (!c) return fail(XT_ERR_ARG, "null ctx");
   if (mode < XT_K_AUTO || mode > XT_K_STORED) return fail(XT_ERR_ARG, "bad exchange mode");
@@ -931,7 +993,16 @@ static int xc_response(xt_ctx* c, int nz) {
       f1.C = Ug[q]; f1.ldc = ldU[q];
       f1.tag = 2;
       RET(gemm(c, f1));
-      if (gga) {
+      if (gga && c->w_kernel && xc_rho_w_lds_bytes(O) <= 160 * 1024) {
+        // dedicated kernel (xt_xcw.hip); tag 4 timing
+        bool prof = false;
+        RET(prof_begin(c, 4, 2.0 * nzg * V * (double)n * O,
+                       8.0 * ((double)nzg * O * V + (double)n * O + 3.0 * n * V + 3.0 * n * nzg), &prof));
+        const int r = xc_rho_w(O, nzg, V, n, PO, nmo, c->zp.p + gr[q].ch0 * chs, (long)nzg * V, V,
+                               PV + compP, compP, nmo, Rg[q], ldR[q], c->st);
+        if (r) return fail(r, "xc_rho_w launch failed");
+        RET(prof_end(c, 4, prof));
+      } else if (gga) {
         GemmDesc f2;   // rhoW[g][xg][c] = sum_a sum_i PhiO0[g][i] Zp[i][xg][a] dPhiV_c[g][a]
         f2.M = 16 * nzg; f2.N = n; f2.K = O; f2.R = nab;
         f2.A = c->zp.p + gr[q].ch0 * chs; f2.sAm = 1; f2.sAk = (long)nzg * V; f2.sAr = 16;
@@ -1009,7 +1080,7 @@ static int xc_response(xt_ctx* c, int nz) {
 // XSF spin-adaptation Delta-A (XSF_TDA.py:1175-1274), ROKS only
 // full-space blocks: rows [0,nc) core / [nc,O) open ; cols [0,no) open / [no,V) virtual
 // ---------------------------------------------------------------------------
-static int xsf_delta_a(xt_ctx* c, int nz) {
+static int xsf_delta_a(xt_ctx* c, int nz, bool skip_k) {
   const xt_desc& d = c->d;
   const int nc = d.nc, no = d.no, nv = d.nv, O = c->O, V = c->V, nmo = d.nmo;
   const long ld = V, sv = (long)O * V, mm = (long)nmo * nmo;
@@ -1059,22 +1130,27 @@ static int xsf_delta_a(xt_ctx* c, int nz) {
       RET(left_mo(c, nz, no, nc, nv, FAh + (long)mo_ * nmo + mc, nmo, 1, Zcv, ld, sv, Sov, ld, sv, -fg * f1));
     }
     // K parts: S_Y += coef * sum_P B[rowsY,rowsX] Z_X B[colsX,colsY]
+    // (skip_k: applied through the stored exchange matrix, exchange_stored_xsf)
     // blocks: cv (rows mc:nc, cols mv:nv) co (mc:nc, mo_:no) ov (mo_:no, mv:nv) oo (mo_:no, mo_:no)
+    if (!skip_k) {
     RET(sandwich(c, B, B, nz, mc, nc, mc, nc, mo_, no, mv, nv, Zco, ld, sv, Scv, ld, sv, -fg * f1));   // cv_co_k
     RET(sandwich(c, B, B, nz, mc, nc, mc, nc, mv, nv, mo_, no, Zcv, ld, sv, Sco, ld, sv, -fg * f1));   // co_cv_k
     RET(sandwich(c, B, B, nz, mc, nc, mo_, no, mv, nv, mv, nv, Zov, ld, sv, Scv, ld, sv, -fg * f1));   // cv_ov_k
     RET(sandwich(c, B, B, nz, mo_, no, mc, nc, mv, nv, mv, nv, Zcv, ld, sv, Sov, ld, sv, -fg * f1));   // ov_cv_k
     RET(sandwich(c, B, B, nz, mc, nc, mo_, no, mv, nv, mo_, no, Zov, ld, sv, Sco, ld, sv, -fg / tsm1)); // co_ov_k
     RET(sandwich(c, B, B, nz, mo_, no, mc, nc, mo_, no, mv, nv, Zco, ld, sv, Sov, ld, sv, -fg / tsm1)); // ov_co_k
+    }
   }
   if (d.sa > 2) {
     const double ff = fg * foo;
+    if (!skip_k) {
     RET(sandwich(c, B, B, nz, mc, nc, mo_, no, mo_, no, mv, nv, Zoo, ld, sv, Scv, ld, sv, -ff * (f2 - 1)));  // cv_oo_k
     RET(sandwich(c, B, B, nz, mo_, no, mc, nc, mv, nv, mo_, no, Zcv, ld, sv, Soo, ld, sv, -ff * (f2 - 1)));  // oo_cv_k
     RET(sandwich(c, B, B, nz, mc, nc, mo_, no, mo_, no, mo_, no, Zoo, ld, sv, Sco, ld, sv, -ff * f3));       // co_oo_k
     RET(sandwich(c, B, B, nz, mo_, no, mc, nc, mo_, no, mo_, no, Zco, ld, sv, Soo, ld, sv, -ff * f3));       // oo_co_k
     RET(sandwich(c, B, B, nz, mc + nc, no, mo_, no, mo_, no, mv, nv, Zoo, ld, sv, Sov, ld, sv, -ff * f3));   // ov_oo_k
     RET(sandwich(c, B, B, nz, mo_, no, mo_, no, mv, nv, mo_, no, Zov, ld, sv, Soo, ld, sv, -ff * f3));       // oo_ov_k
+    }
     if (loc) {
       // fA_co = FAh[mc+i][mo_+w] ; fB_vo = FBh[mv+a][mo_+v]
       RET(left_mo(c, nz, nc, no, no, FAh + (long)mc * nmo + mo_, nmo, 1, Zoo, ld, sv, Sco, ld, sv, -ff * f3));
@@ -1129,10 +1205,12 @@ extern "C" int xt_apply(xt_ctx* c, int nz, const double* z, double* sigma, int p
   else if (xsf) xsf_assemble(c->st, nz, d.nc, d.no, d.nv, d.remove, c->vects.p, zd, c->ze.p);
   else HIPCHK(hipMemcpyAsync(c->ze.p, zd, chs * 8, hipMemcpyDeviceToDevice, c->st));
   HIPCHK(hipMemsetAsync(c->acc.p, 0, nch * chs * 8, c->st));
-  // Zp gets 32 zeroed doubles of slack: the fused rho-forward GEMM reads whole
-  // 16-wide a-blocks, up to 15 past the last channel's V (weighted by zero)
-  RET(c->zp.ensure(nch * chs + 32));
-  HIPCHK(hipMemsetAsync(c->zp.p + nch * chs, 0, 32 * 8, c->st));
+  // Zp gets zeroed slack: the fused rho-forward kernels read whole a-tiles (up to 31
+  // columns past the last channel's V, weighted by zero) and whole 8-row occupied
+  // blocks (up to 7 rows of nch nz V past O, multiplied by zero PhiO rows)
+  const long zslack = 8L * nch * nz * V + 64;
+  RET(c->zp.ensure(nch * chs + zslack));
+  HIPCHK(hipMemsetAsync(c->zp.p + nch * chs, 0, zslack * 8, c->st));
   RET(c->accT.ensure(nch * chs));
   HIPCHK(hipMemsetAsync(c->accT.p, 0, nch * chs * 8, c->st));
   Group grp[2];
@@ -1185,6 +1263,7 @@ extern "C" int xt_apply(xt_ctx* c, int nz, const double* z, double* sigma, int p
 
   // ---- Coulomb / exchange ----------------------------------------------------
   const bool has_k = (c->ck != 0.0 || c->ck_lr != 0.0);
+  bool xsf_k_done = false;   // Delta-A exchange already applied through the stored matrix
   if (d.naux > 0) {
     if (!sf && naux_w(c) > 0) {   // J (spin-conserving only)
       RET(c->gam.ensure((size_t)nz * naux_w(c)));
@@ -1199,13 +1278,18 @@ extern "C" int xt_apply(xt_ctx* c, int nz, const double* z, double* sigma, int p
       RET(resolve_kmode(c));
       if (c->k_resolved == 1) {
         if (!c->kx_valid) RET(build_kx(c));
-        RET(exchange_stored(c, nz));
+        if (xsf_fused_k(c)) {
+          RET(exchange_stored_xsf(c, nz));
+          xsf_k_done = true;
+        } else {
+          RET(exchange_stored(c, nz));
+        }
       } else {
         RET(exchange_main(c, nz, c->Bmo, -c->ck));
         if (c->ck_lr != 0.0) RET(exchange_main(c, nz, c->Bmo_lr, -c->ck_lr));
       }
     }
-    if (xsf && d.sa > 0 && naux_w(c) > 0) RET(xsf_delta_a(c, nz));
+    if (xsf && d.sa > 0 && naux_w(c) > 0) RET(xsf_delta_a(c, nz, xsf_k_done));
   }
   HIPCHK(hipEventRecord(c->ev[2], c->st));
 

@@ -32,17 +32,24 @@ namespace xt {
 typedef double d4x __attribute__((ext_vector_type(4)));
 typedef double d2x __attribute__((ext_vector_type(2)));
 
-constexpr int SK_MP = 48;        // padded rows (3 MFMA sub-tiles)
-constexpr int SK_TM = 3;
-constexpr int SK_TN = 4;         // 16-column sub-tiles per wave
+// Two shapes: <3, 4, 64> (M <= 48: the X-TDA / SF exchange, 2 nz or nz rows; two
+// blocks per CU) and <10, 2, 32> (M <= 160: the XSF exchange with its four
+// spin-adaptation source blocks, 4 nz rows; one block per CU, 160 accumulator VGPRs).
 constexpr int SK_WAVES = 8;
-constexpr int SK_BN = 16 * SK_TN * SK_WAVES;   // 512 columns per block
-constexpr int SK_BK = 64;        // k per LDS chunk (16 k-steps)
-constexpr int SK_D = 4;          // B prefetch depth (k-steps)
+constexpr int SK_MAXM = 160;
 
-__global__ void __launch_bounds__(512, 2)
+// SK_D: B prefetch ring depth in k-steps (Kx streams from HBM: the ring has to
+// cover an HBM miss under full load, ~2-4 us, with 8 waves per CU)
+template <int SK_TM, int SK_TN, int SK_BK, int SK_D>
+__global__ void __launch_bounds__(512, SK_TM <= 3 ? 2 : 1)
 k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
          const double* __restrict__ B, long ldb, double* __restrict__ out, long ldo) {
+  constexpr int SK_MP = 16 * SK_TM;                // padded rows
+  constexpr int SK_BN = 16 * SK_TN * SK_WAVES;     // columns per block
+  constexpr int A_PIECES = SK_BK * SK_MP / 2;      // 16-B pieces per chunk
+  static_assert(A_PIECES % 512 == 0, "A staging map");
+  constexpr int A_E = A_PIECES / 512;
+  static_assert((SK_BK / 4) % SK_D == 0, "ring slots");
   __shared__ __attribute__((aligned(16))) double As[2][SK_BK * SK_MP];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -51,11 +58,11 @@ k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
   const int k0 = split * kchunk;
   const int k1 = (k0 + kchunk < K) ? k0 + kchunk : K;
   const int nw = strip * SK_BN + wave * (16 * SK_TN);
-  // this lane's 4 physical columns c0 .. c0 + 3.  Rows are readable up to ldb
-  // (a multiple of 4 >= N, zero padding), so a lane with c0 < N loads its 4
-  // columns whole; lanes past N load the last 4 columns and store nothing.
-  const int c0 = nw + 4 * r;
-  const int cl = c0 + 4 <= (int)ldb ? c0 : (int)ldb - 4;
+  // this lane's SK_TN physical columns c0 .. c0 + SK_TN - 1.  Rows are readable up
+  // to ldb (a multiple of 4 >= N, zero padding), so a lane with c0 < N loads its
+  // columns whole; lanes past N load the last ones and store nothing.
+  const int c0 = nw + SK_TN * r;
+  const int cl = c0 + SK_TN <= (int)ldb ? c0 : (int)ldb - SK_TN;
   const int nchunks = (k1 - k0 + SK_BK - 1) / SK_BK;
 
   d4x acc[SK_TM][SK_TN];
@@ -64,14 +71,14 @@ k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
 #pragma unroll
     for (int j = 0; j < SK_TN; ++j) acc[i][j] = (d4x){0.0, 0.0, 0.0, 0.0};
 
-  // A chunk staging: 64 k x 48 m doubles = 1536 16-B pieces, 3 per thread; rows
-  // past this split's k1 are zero, which makes whole 16-step chunks safe at the end
-  d2x ra[3];
+  // A chunk staging: SK_BK k x SK_MP m doubles in 16-B pieces, A_E per thread; rows
+  // past this split's k1 are zero, which makes whole chunks safe at the end
+  d2x ra[A_E];
   auto load_a = [&](int ch) XT_INLINE {
 #pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      const int piece = tid + 512 * e;             // 0..1535
-      const int kk = piece / 24, mm = 2 * (piece % 24);
+    for (int e = 0; e < A_E; ++e) {
+      const int piece = tid + 512 * e;
+      const int kk = piece / (SK_MP / 2), mm = 2 * (piece % (SK_MP / 2));
       const int k = k0 + ch * SK_BK + kk;
       const d2x v = *(const d2x*)(AT + (long)(k < K ? k : K - 1) * SK_MP + mm);
       ra[e] = k < k1 ? v : (d2x){0.0, 0.0};
@@ -79,21 +86,26 @@ k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
   };
   auto store_a = [&](int buf) XT_INLINE {
 #pragma unroll
-    for (int e = 0; e < 3; ++e) {
+    for (int e = 0; e < A_E; ++e) {
       const int piece = tid + 512 * e;
-      *(d2x*)(&As[buf][(piece / 24) * SK_MP + 2 * (piece % 24)]) = ra[e];
+      *(d2x*)(&As[buf][(piece / (SK_MP / 2)) * SK_MP + 2 * (piece % (SK_MP / 2))]) = ra[e];
     }
   };
   // B: k-step s of this split -> row k0 + 4 s + q, clamped to K - 1 (those rows
   // meet zero A rows); branch-free so the loads pipeline across k-steps
-  auto load_b = [&](int s, d4x& v) XT_INLINE {
+  typedef double bvec __attribute__((ext_vector_type(SK_TN)));
+  auto load_b = [&](int s, bvec& v) XT_INLINE {
     const int k = k0 + 4 * s + q;
     const double* p = B + (long)(k < K ? k : K - 1) * ldb + cl;
-    const d2x lo = *(const d2x*)p, hi = *(const d2x*)(p + 2);
-    v = (d4x){lo[0], lo[1], hi[0], hi[1]};
+    if constexpr (SK_TN == 4) {
+      const d2x lo = *(const d2x*)p, hi = *(const d2x*)(p + 2);
+      v = (bvec){lo[0], lo[1], hi[0], hi[1]};
+    } else {
+      v = *(const d2x*)p;
+    }
   };
 
-  d4x bq[SK_D];
+  bvec bq[SK_D];
 #pragma unroll
   for (int t = 0; t < SK_D; ++t) load_b(t, bq[t]);
   load_a(0);
@@ -112,7 +124,7 @@ k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
         double af[SK_TM];
 #pragma unroll
         for (int i = 0; i < SK_TM; ++i) af[i] = As[buf][kk * SK_MP + 16 * i + r];
-        const d4x bv = bq[u];
+        const bvec bv = bq[u];
         load_b(s + SK_D, bq[u]);                     // refill this ring slot
 #pragma unroll
         for (int i = 0; i < SK_TM; ++i)
@@ -127,7 +139,7 @@ k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
     store_a(buf ^ 1);
     __syncthreads();
   }
-  // C/D layout: col = lane & 15 (= r), row = 4 reg + q; sub-tile j col r -> 4 r + j
+  // C/D layout: col = lane & 15 (= r), row = 4 reg + q; sub-tile j col r -> TN r + j
   if (c0 >= N) return;
   double* o = out + (long)split * SK_MP * ldo;
 #pragma unroll
@@ -135,12 +147,12 @@ k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int m = 16 * i + q + 4 * t;
-      d4x v;
+      bvec v;
 #pragma unroll
       for (int j = 0; j < SK_TN; ++j) v[j] = acc[i][j][t];
-      if (c0 + 3 < N) {
-        *(d2x*)(o + (long)m * ldo + c0) = (d2x){v[0], v[1]};
-        *(d2x*)(o + (long)m * ldo + c0 + 2) = (d2x){v[2], v[3]};
+      if (c0 + SK_TN - 1 < N) {
+#pragma unroll
+        for (int j = 0; j < SK_TN; j += 2) *(d2x*)(o + (long)m * ldo + c0 + j) = (d2x){v[j], v[j + 1]};
       } else {
 #pragma unroll
         for (int j = 0; j < SK_TN; ++j) if (c0 + j < N) o[(long)m * ldo + c0 + j] = v[j];
@@ -149,65 +161,82 @@ k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
 }
 
 // C[m][n] = alpha * sum_s part[s][m][n] + beta * C[m][n]  (fixed summation order)
-__global__ void k_skinny_reduce(int M, int N, int nsplit, const double* __restrict__ part, long ldp,
+__global__ void k_skinny_reduce(int M, int N, int nsplit, int MP, const double* __restrict__ part, long ldp,
                                 double alpha, double beta, double* __restrict__ C, long ldc) {
   const long total = (long)M * N;
   for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
     const int m = (int)(t / N), n = (int)(t % N);
     double acc = 0.0;
-    for (int s = 0; s < nsplit; ++s) acc += part[((long)s * SK_MP + m) * ldp + n];
+    for (int s = 0; s < nsplit; ++s) acc += part[((long)s * MP + m) * ldp + n];
     double* c = C + (long)m * ldc + n;
     *c = alpha * acc + (beta != 0.0 ? beta * (*c) : 0.0);
   }
 }
 
-// A (M x K, row stride lda) -> AT (K x 48), zero-padded rows m >= M
-__global__ void k_skinny_transpose(int M, int K, const double* __restrict__ A, long lda, double* __restrict__ AT) {
-  const long total = (long)K * SK_MP;
+// A (M x K, row stride lda) -> AT (K x MP), zero-padded rows m >= M
+__global__ void k_skinny_transpose(int M, int K, int MP, const double* __restrict__ A, long lda,
+                                   double* __restrict__ AT) {
+  const long total = (long)K * MP;
   for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const int k = (int)(t / SK_MP), m = (int)(t % SK_MP);
+    const int k = (int)(t / MP), m = (int)(t % MP);
     AT[t] = m < M ? A[(long)m * lda + k] : 0.0;
   }
 }
 
-int skinny_splits(int N, int K);
-
-size_t skinny_workspace_bytes(int M, int N, int K) {
-  (void)M;
-  const int nsplit = skinny_splits(N, K);
-  return sizeof(double) * ((size_t)K * SK_MP + (size_t)nsplit * SK_MP * N);
+namespace {
+struct SkShape { int mp, bn, bk, slots; };
+// (padded rows, columns per block, k per chunk, concurrent blocks per CU)
+SkShape sk_shape(int M) {
+  if (M <= 48) return {48, 16 * 4 * SK_WAVES, 64, 2};
+  return {160, 16 * 2 * SK_WAVES, 32, 1};
 }
+}  // namespace
 
-int skinny_splits(int N, int K) {
-  const int strips = (N + SK_BN - 1) / SK_BN;
-  int s = (2 * 256 + strips - 1) / strips;        // >= two blocks per CU over the chip
-  const int max_s = (K + 4 * SK_BK - 1) / (4 * SK_BK);   // keep >= 4 chunks per split
+static int skinny_splits_m(int M, int N, int K) {
+  const SkShape sh = sk_shape(M);
+  const int strips = (N + sh.bn - 1) / sh.bn;
+  int s = (sh.slots * 256 + strips - 1) / strips;        // >= the chip's block slots
+  const int max_s = (K + 4 * sh.bk - 1) / (4 * sh.bk);   // keep >= 4 chunks per split
   if (s > max_s) s = max_s;
   return s < 1 ? 1 : s;
+}
+
+int skinny_splits(int N, int K) { return skinny_splits_m(48, N, K); }
+
+size_t skinny_workspace_bytes(int M, int N, int K) {
+  const SkShape sh = sk_shape(M);
+  const int nsplit = skinny_splits_m(M, N, K);
+  return sizeof(double) * ((size_t)K * sh.mp + (size_t)nsplit * sh.mp * N);
 }
 
 int skinny_gemm(int M, int N, int K, double alpha, const double* A, long lda, const double* B, long ldb,
                 double beta, double* C, long ldc, double* ws, size_t ws_bytes, hipStream_t st) {
   if (M <= 0 || N <= 0) return 0;
-  if (M > SK_MP || N < 4 || K <= 0) return XT_ERR_ARG;
+  if (M > SK_MAXM || N < 4 || K <= 0) return XT_ERR_ARG;
   if (ws_bytes < skinny_workspace_bytes(M, N, K)) return XT_ERR_ARG;
   // 16-B aligned rows, readable (zero-padded) up to column ldb >= N rounded up to 4
   if ((ldb & 3) || ldb < ((N + 3) & ~3) || (reinterpret_cast<size_t>(B) & 15)) return XT_ERR_ARG;
-  if (K > (1 << 30) / SK_MP) return XT_ERR_ARG;
-  const int nsplit = skinny_splits(N, K);
+  const SkShape sh = sk_shape(M);
+  if (K > (1 << 30) / sh.mp) return XT_ERR_ARG;
+  const int nsplit = skinny_splits_m(M, N, K);
   int kchunk = (K + nsplit - 1) / nsplit;
-  kchunk = ((kchunk + SK_BK - 1) / SK_BK) * SK_BK;
+  kchunk = ((kchunk + sh.bk - 1) / sh.bk) * sh.bk;
   double* AT = ws;
-  double* part = ws + (size_t)K * SK_MP;
-  const long tot = (long)K * SK_MP;
+  double* part = ws + (size_t)K * sh.mp;
+  const long tot = (long)K * sh.mp;
   hipLaunchKernelGGL(k_skinny_transpose, dim3((unsigned)((tot + 255) / 256 < 65536 ? (tot + 255) / 256 : 65536)),
-                     dim3(256), 0, st, M, K, A, lda, AT);
-  const int strips = (N + SK_BN - 1) / SK_BN;
+                     dim3(256), 0, st, M, K, sh.mp, A, lda, AT);
+  const int strips = (N + sh.bn - 1) / sh.bn;
   const int used = (K + kchunk - 1) / kchunk;
-  hipLaunchKernelGGL(k_skinny, dim3(strips, used), dim3(512), 0, st, N, K, kchunk, AT, B, ldb, part, (long)N);
+  if (sh.mp == 48)
+    hipLaunchKernelGGL((k_skinny<3, 4, 64, 4>), dim3(strips, used), dim3(512), 0, st, N, K, kchunk, AT, B, ldb, part,
+                       (long)N);
+  else
+    hipLaunchKernelGGL((k_skinny<10, 2, 32, 4>), dim3(strips, used), dim3(512), 0, st, N, K, kchunk, AT, B, ldb,
+                       part, (long)N);
   const long mn = (long)M * N;
   hipLaunchKernelGGL(k_skinny_reduce, dim3((unsigned)((mn + 255) / 256 < 8192 ? (mn + 255) / 256 : 8192)),
-                     dim3(256), 0, st, M, N, used, part, (long)N, alpha, beta, C, ldc);
+                     dim3(256), 0, st, M, N, used, sh.mp, part, (long)N, alpha, beta, C, ldc);
   return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
 }
 

@@ -68,7 +68,7 @@ void plan_gemm(const GemmDesc& d, GemmParams* p, int* cfg);
 // skinny streaming GEMM (xt_exch.hip): C = alpha A B + beta C for M <= 48 rows,
 // B (K x N, 16-B aligned rows of stride ldb: a multiple of 4 >= N, the padding
 // readable) streamed once from HBM
-constexpr int SKINNY_MAX_M = 48;
+constexpr int SKINNY_MAX_M = 160;   // 48-row tile up to 48 rows, 160-row tile beyond
 int skinny_splits(int N, int K);
 size_t skinny_workspace_bytes(int M, int N, int K);
 int skinny_gemm(int M, int N, int K, double alpha, const double* A, long lda, const double* B, long ldb,
@@ -81,6 +81,12 @@ constexpr int XC_GRID_SLACK = 64;
 size_t xc_back_m_workspace_bytes(int O, int nx, int V, int n);
 int xc_back_m(int O, int nx, int V, int n, const double* PO, long ldp, const double* W, long wc, long wg,
               const double* R, long rg, double* C, long ldc, double* ws, size_t ws_bytes, hipStream_t st);
+// dedicated XC rho-forward (xt_xcw.hip): rhoW[g][xg][c] = sum_a dPhiV_c[g][a] sum_i
+// PhiO[g][i] Zp[i zi + xg zx + a]; reads Zp up to 7 rows past O and WA - 1 columns past
+// V (zeroed slack), grid arrays XC_GRID_SLACK rows past n
+size_t xc_rho_w_lds_bytes(int O);
+int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const double* Z, long zi, long zx,
+             const double* W, long wc, long wg, double* R, long rg, hipStream_t st);
 size_t dgemm_workspace_bytes(const GemmDesc& d);
 int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes);
 

@@ -20,6 +20,13 @@ void xc_uks_w(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O
 void xc_sf(hipStream_t st, int G, int g0, int nz, int O, int nmo, const double* phio, const double* fsf, double* U);
 void weight_fxc(hipStream_t st, long n4, int ngrid, const double* w, double* f);
 void xsf_assemble(hipStream_t st, int nz, int nc, int no, int nv, int remove, const double* vects, const double* z, double* ze);
+// XSF exchange through the stored matrix: the trial vectors split into their four
+// spin-adaptation source blocks (cv, co, ov, oo), and the per-block results combined
+// with a 4 x 4 weight table w16[source][target]
+void xsf_split4(hipStream_t st, int nz, int O, int V, int nc, int no, const double* ze, double* zb);
+struct W16 { double w[16]; };   // w[4 source + target]
+void xsf_combine4(hipStream_t st, int nz, int O, int V, int nc, int no, const W16& w16, const double* yb,
+                  double* acc);
 void xsf_extract(hipStream_t st, int nz, int nc, int no, int nv, int remove, const double* vects, const double* full, double* out);
 void xsf_jdiag(hipStream_t st, int naux, int nmo, int nc, int no, int nv, const double* bmo, double* co_j, double* ov_j);
 void precond(hipStream_t st, int nrow, int dim, const double* diag, const double* e, double shift, const double* r, double* out);

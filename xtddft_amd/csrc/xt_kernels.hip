@@ -677,6 +677,40 @@ void permute_add_strided(hipStream_t st, int nz, int nry, int ncy, double alpha,
   hipLaunchKernelGGL(k_permute_add_strided, dim3(nblocks((long)nz * nry * ncy)), dim3(256), 0, st,
                      nz, nry, ncy, alpha, src, dst, ldS, svS);
 }
+// XSF superset blocks (rows [0,nc) core / [nc,O) open; cols [0,no) open / [no,V) virtual):
+// 0 cv, 1 co, 2 ov, 3 oo
+__device__ __forceinline__ int xsf_block(int i, int a, int nc, int no) {
+  return (i < nc ? 0 : 2) + (a < no ? 1 : 0);
+}
+
+// zb[X nz + x][(i,a)] = ze[x][(i,a)] if (i,a) is in block X else 0   (4 nz rows)
+__global__ void k_xsf_split4(int nz, int O, int V, int nc, int no, const double* __restrict__ ze,
+                             double* __restrict__ zb) {
+  const long ov = (long)O * V, total = 4L * nz * ov;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const long e = t % ov;
+    const int row = (int)(t / ov), X = row / nz, x = row % nz;
+    const int i = (int)(e / V), a = (int)(e % V);
+    zb[t] = xsf_block(i, a, nc, no) == X ? ze[(long)x * ov + e] : 0.0;
+  }
+}
+
+// acc[x][(i,a)] += sum_X w[X][Y(i,a)] yb[X nz + x][(i,a)]
+__global__ void k_xsf_combine4(int nz, int O, int V, int nc, int no, W16 w16,
+                               const double* __restrict__ yb, double* __restrict__ acc) {
+  const long ov = (long)O * V, total = (long)nz * ov;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const long e = t % ov;
+    const int x = (int)(t / ov);
+    const int i = (int)(e / V), a = (int)(e % V);
+    const int Y = xsf_block(i, a, nc, no);
+    double s = 0.0;
+#pragma unroll
+    for (int X = 0; X < 4; ++X) s += w16.w[4 * X + Y] * yb[((long)X * nz + x) * ov + e];
+    acc[t] += s;
+  }
+}
+
 void xsf_rank1(hipStream_t st, int nz, int nc, int no, int nv, int nmo, double a2, double a4,
                const double* ze, const double* fs, const double* fa, const double* fb, double* acc) {
   hipLaunchKernelGGL(k_xsf_rank1, dim3(nz), dim3(256), 0, st, nz, nc, no, nv, nmo, a2, a4, ze, fs, fa, fb, acc);
@@ -744,4 +778,15 @@ void row_scale(hipStream_t st, int nrow, int dim, double* x, const double* s) {
   hipLaunchKernelGGL(k_row_scale, dim3(nblocks((long)nrow * dim)), dim3(256), 0, st, nrow, dim, x, s);
 }
 
+}  // namespace xt
+
+namespace xt {
+void xsf_split4(hipStream_t st, int nz, int O, int V, int nc, int no, const double* ze, double* zb) {
+  hipLaunchKernelGGL(k_xsf_split4, dim3(nblocks(4L * nz * O * V)), dim3(256), 0, st, nz, O, V, nc, no, ze, zb);
+}
+void xsf_combine4(hipStream_t st, int nz, int O, int V, int nc, int no, const W16& w16, const double* yb,
+                  double* acc) {
+  hipLaunchKernelGGL(k_xsf_combine4, dim3(nblocks((long)nz * O * V)), dim3(256), 0, st, nz, O, V, nc, no, w16, yb,
+                     acc);
+}
 }  // namespace xt

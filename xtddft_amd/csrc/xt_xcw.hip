@@ -1,0 +1,226 @@
+// XC rho-forward (W route) as a dedicated kernel: the gradient-of-virtual half of
+// the transition-density gradient that nr_uks_fxc contracts (XTDA.py:514):
+//
+//   rhoW[g][xg][c] = sum_a dPhiV_c[g][a] * sum_i PhiO[g][i] * Zp[i][xg][a]     (c < 3)
+//
+// The intermediate T[g][xg][a] = sum_i PhiO Zp (nx V values per grid point) never
+// leaves registers.  MFMA orientation: rows = virtuals a, columns = grid points g,
+// K = occupied i.  Each wave owns one trial pair xg and 16 TNG grid points:
+//   * A = Zp[i][xg][a] (16 contiguous a per fragment row): loaded straight from
+//     global memory into registers through a 4-k-step ring (each wave's own xg);
+//   * B = PhiO[g][i]: the block's 16 TNG x O tile, loaded ONCE per block into LDS
+//     and resident for the whole a loop;
+//   * after each 32-wide a-tile's K loop the accumulators T[a][g] are contracted
+//     with dPhiV_c[g][a] (staged per a-tile in LDS, shared by the 8 waves) into
+//     per-lane partial sums racc[j][c] -- the sum over a stays in-lane (rows a of a
+//     lane are q + 4 reg + 16 t) and only the final 4-row reduction crosses lanes,
+//     once per block.
+// One barrier per a-tile (26 k-steps x 8 MFMAs per wave at O = 101).
+// LDS images are [row][g] with g XOR-swizzled by h(row) = (row & 15) | (row & 1) << 4:
+// the global loads run along the row index (coalesced), so 16 lanes of a
+// ds_write_b64 group write 16 consecutive rows at one g -> 16 distinct bank pairs;
+// the fragment / weight reads (16 consecutive g, two rows of opposite parity per
+// 32-lane group) land in opposite bank halves.
+#include <hip/hip_runtime.h>
+#include "xt_internal.h"
+
+namespace xt {
+
+#define XT_INLINE __attribute__((always_inline))
+typedef double d4w __attribute__((ext_vector_type(4)));
+
+constexpr int WA = 32;           // virtuals per a-tile (2 MFMA row sub-tiles)
+constexpr int TMA = WA / 16;
+constexpr int WXB = 8;           // trial pairs per block (one per wave)
+constexpr int ZD = 2;            // Zp prefetch ring depth (k-steps; divides KS = KI / 4)
+
+__device__ __forceinline__ int swz(int row) { return (row & 15) | ((row & 1) << 4); }
+
+// transposing 4-row sum (lanes l, l^16, l^32, l^48): every lane ends with the total
+__device__ __forceinline__ double rows4(double v) {
+  auto pair = [](double x, bool p32) XT_INLINE {
+    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+    const auto a = p32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                       : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = p32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                       : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+  };
+  return pair(pair(v, false), true);
+}
+
+template <int TNG>
+__global__ void __launch_bounds__(512, 1)
+k_xc_rho_w(int O, int nx, int V, int n,
+           const double* __restrict__ PO, long ldp,
+           const double* __restrict__ Z, long zi, long zx,
+           const double* __restrict__ Wg, long wc, long wg,
+           double* __restrict__ Rout, long rg) {
+  constexpr int GB = 16 * TNG;                 // grid points per block
+  constexpr int W_IMG = 3 * WA * GB;           // one weight buffer (doubles)
+  constexpr int W_LD = W_IMG / 512;            // weight elements staged per thread
+  static_assert(W_IMG % 512 == 0, "weight staging map");
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int KI = (O + 7) & ~7;                 // occupied rows in the image (k-steps even)
+  double* sP = sm;                             // [KI][GB]
+  double* sW = sm + KI * GB;                   // [2][3][WA][GB]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4, r16 = lane & 15;
+
+  // block -> (xg-set, g-tile), g-tile fastest within an XCD's contiguous range: the
+  // blocks resident on one XCD share the xg-set's Zp slice in its L2
+  const int ntg = (n + GB - 1) / GB;
+  const int nblk = gridDim.x;
+  int lid = blockIdx.x;
+  {
+    const int xcd = lid & 7, idx = lid >> 3, qn = nblk >> 3, rem = nblk & 7;
+    lid = xcd * qn + (xcd < rem ? xcd : rem) + idx;
+  }
+  const int gt = lid % ntg, xs = lid / ntg;
+  const int g0 = gt * GB, x0 = xs * WXB;
+  const int xg = x0 + wave;
+  const bool wave_on = xg < nx;
+  const int nat = (V + WA - 1) / WA;
+  const int KS = KI / 4;
+
+  // ---- PhiO tile -> LDS (once) ----------------------------------------------
+  for (int p = tid; p < KI * GB; p += 512) {
+    const int g = p / KI, i = p % KI;
+    const double v = i < O ? PO[(long)(g0 + g) * ldp + i] : 0.0;   // rows past n: zeroed slack
+    sP[i * GB + (g ^ swz(i))] = v;
+  }
+  // ---- weights of a-tile `at` (global -> registers -> LDS) -------------------
+  double rw[W_LD];
+  auto load_w = [&](int at) XT_INLINE {
+#pragma unroll
+    for (int e = 0; e < W_LD; ++e) {
+      const int p = tid + 512 * e, c = p / (WA * GB), g = (p / WA) % GB, a = p % WA;
+      rw[e] = Wg[c * wc + (long)(g0 + g) * wg + min(at * WA + a, V - 1)];
+    }
+  };
+  auto store_w = [&](int buf, int at) XT_INLINE {
+#pragma unroll
+    for (int e = 0; e < W_LD; ++e) {
+      const int p = tid + 512 * e, c = p / (WA * GB), g = (p / WA) % GB, a = p % WA;
+      sW[buf * W_IMG + (c * WA + a) * GB + (g ^ swz(a))] = at * WA + a < V ? rw[e] : 0.0;
+    }
+  };
+  load_w(0);
+  store_w(0, 0);
+
+  // ---- Zp ring: k-step u of the whole a loop (a-tile u / KS, k-step u % KS) ----
+  // lane (q, r16) loads rows i = 4 s + q (past O: zeroed slack rows of Zp) of
+  // columns at WA + 16 t + r16 (past V: the next pair's values, weighted by zero)
+  const double* zb = Z + (long)(wave_on ? xg : 0) * zx + r16 + (long)q * zi;
+  double zq[ZD][TMA];
+  int zu_at = 0, zu_s = 0;                     // next k-step to load
+  auto load_z = [&](int slot) XT_INLINE {
+    const double* p = zb + (long)(4 * zu_s) * zi + zu_at * WA;
+#pragma unroll
+    for (int t = 0; t < TMA; ++t) zq[slot][t] = p[16 * t];
+    if (++zu_s == KS) { zu_s = 0; zu_at = zu_at + 1 < nat ? zu_at + 1 : zu_at; }
+  };
+#pragma unroll
+  for (int d = 0; d < ZD; ++d) load_z(d);
+
+  d4w acc[TMA][TNG];
+  double racc[TNG][3];
+#pragma unroll
+  for (int j = 0; j < TNG; ++j)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) racc[j][c] = 0.0;
+
+  const int p_lane = q * GB;                   // B image: row 4 s + q, column (16 j + r16) ^ swz
+  __syncthreads();
+  for (int at = 0; at < nat; ++at) {
+    const int buf = at & 1;
+    if (at + 1 < nat) load_w(at + 1);
+#pragma unroll
+    for (int t = 0; t < TMA; ++t)
+#pragma unroll
+      for (int j = 0; j < TNG; ++j) acc[t][j] = (d4w){0.0, 0.0, 0.0, 0.0};
+    if (wave_on) {
+      // K loop over the occupied rows, ZD k-steps per unrolled body (static ring slots)
+      for (int s0 = 0; s0 < KS; s0 += ZD) {
+#pragma unroll
+        for (int d = 0; d < ZD; ++d) {
+          const int s = s0 + d;
+          const int i = 4 * s + q;
+          const int sw = swz(i);
+          double bf[TNG];
+#pragma unroll
+          for (int j = 0; j < TNG; ++j) bf[j] = sP[p_lane + 4 * s * GB + ((16 * j + r16) ^ sw)];
+          double af[TMA];
+#pragma unroll
+          for (int t = 0; t < TMA; ++t) af[t] = zq[d][t];
+          load_z(d);
+#pragma unroll
+          for (int t = 0; t < TMA; ++t)
+#pragma unroll
+            for (int j = 0; j < TNG; ++j)
+              acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t], bf[j], acc[t][j], 0, 0, 0);
+        }
+      }
+      // contraction with the a-tile's weights: acc[t][j][r] = T[a = 16 t + q + 4 r][g = 16 j + r16]
+      const double* w = sW + buf * W_IMG;
+#pragma unroll
+      for (int t = 0; t < TMA; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int a = 16 * t + q + 4 * r;
+          const int sa = swz(a);
+#pragma unroll
+          for (int j = 0; j < TNG; ++j) {
+            const int col = (16 * j + r16) ^ sa;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) racc[j][c] += acc[t][j][r] * w[(c * WA + a) * GB + col];
+          }
+          // one row at a time: unfenced, the compiler hoists all 96 weight reads
+          // ahead of the FMAs and spills
+          __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (at + 1 < nat) store_w(buf ^ 1, at + 1);
+    __syncthreads();
+  }
+  if (!wave_on) return;
+#pragma unroll
+  for (int j = 0; j < TNG; ++j) {
+    const int g = g0 + 16 * j + r16;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const double v = rows4(racc[j][c]);
+      if (q == 0 && g < n) Rout[(long)g * rg + 3 * xg + c] = v;
+    }
+  }
+}
+
+static constexpr int kWTng = 4;
+
+size_t xc_rho_w_lds_bytes(int O) {
+  const int GB = 16 * kWTng;
+  return sizeof(double) * ((size_t)((O + 7) & ~7) * GB + 2 * 3 * WA * GB);
+}
+
+int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const double* Z, long zi, long zx,
+             const double* W, long wc, long wg, double* R, long rg, hipStream_t st) {
+  if (O <= 0 || nx <= 0 || V <= 0 || n <= 0) return 0;
+  const size_t lds = xc_rho_w_lds_bytes(O);
+  if (lds > 160 * 1024) return XT_ERR_ARG;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_xc_rho_w<kWTng>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
+  const int GB = 16 * kWTng;
+  const int blocks = ((n + GB - 1) / GB) * ((nx + WXB - 1) / WXB);
+  hipLaunchKernelGGL(k_xc_rho_w<kWTng>, dim3(blocks), dim3(512), lds, st, O, nx, V, n, PO, ldp, Z, zi, zx, W,
+                     wc, wg, R, rg);
+  return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
+}
+
+}  // namespace xt
