@@ -1,2 +1,2 @@
-static const char id[] = "XT_BUILD_ID:fc005ff7614c737b4068ab3aa11c8b7d";
+static const char id[] = "XT_BUILD_ID:a21fb5f85ca3b3cf17bd0ed0d2367112";
 const char* xt_build_id(void) { return id + 12; }
