@@ -1,0 +1,74 @@
+"""GPU: the alternative kernel paths each context can select (environment, read at
+xt_create) against the oracle, and the XSF exchange through the stored matrix at
+the row counts that take its 160-row streaming tile and its batching.
+
+* XT_M_KERNEL=0  -> XC M-backward through the generic engine's mode 2
+  (default: the dedicated kernel, xt_xcm.hip)
+* XT_W_KERNEL=1  -> XC rho-forward through the dedicated kernel (xt_xcw.hip)
+  (default: the engine's mode 1)
+* XT_XSF_FUSED=0 -> XSF Delta-A exchange as direct DF sandwiches
+  (default with the stored exchange: one Kx stream for main + Delta-A exchange)
+Tolerance: 1e-12 relative max-norm on sigma (FP64 round-off of a different
+summation order), as in test_gpu_parity.py.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import xsf_tda as oxsf
+from oracle import xtda as oxtda
+from xtddft_amd.synthetic import make_mf, make_trial_vectors
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-12
+
+
+def rel(a, b):
+    return np.abs(a - b).max() / np.abs(b).max()
+
+
+@pytest.fixture
+def env():
+    saved = {}
+
+    def set_(**kw):
+        for k, v in kw.items():
+            saved.setdefault(k, os.environ.get(k))
+            os.environ[k] = str(v)
+    yield set_
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+
+
+@pytest.mark.parametrize("knobs", [dict(XT_M_KERNEL=0), dict(XT_W_KERNEL=1), dict(XT_M_KERNEL=0, XT_W_KERNEL=1)])
+@pytest.mark.parametrize("nc,no,nao", [(5, 2, 26), (33, 1, 60), (95, 2, 130), (120, 3, 150)])
+def test_xc_kernel_variants(hiplib, env, knobs, nc, no, nao):
+    """O = 7, 34, 97 and 123: one to eight 16-row sub-tiles of the dedicated kernels."""
+    from xtddft_amd.operator import DeviceOperator
+    env(**knobs)
+    mf = make_mf(nao=nao, nc=nc, no=no, ngrid=3000, xctype="GGA", hyb=0.2)
+    vind, hdiag = oxtda.gen_tda_operation(mf)
+    z = make_trial_vectors(7, hdiag.size)
+    op = DeviceOperator(mf, "XTDA")
+    assert rel(op.apply(z), vind(z)) < RTOL
+
+
+@pytest.mark.parametrize("nz", [13, 41])
+@pytest.mark.parametrize("sa", [2, 3])
+@pytest.mark.parametrize("fused", [1, 0])
+def test_xsf_stored_exchange_blocks(hiplib, env, nz, sa, fused):
+    """4 nz = 52 rows (160-row tile) and 41 vectors (one 40-vector batch + 1)."""
+    from xtddft_amd.operator import DeviceOperator
+    env(XT_XSF_FUSED=fused)
+    mf = make_mf(nao=30, nc=6, no=3, xctype="GGA", hyb=0.5)
+    o = oxsf.XSFOracle(mf, SA=sa)
+    fg = oxsf.default_fglobal(mf)
+    vind, hdiag = o.gen_tda_operation_sf(foo=0.7, fglobal=fg)
+    z = make_trial_vectors(nz, hdiag.size)
+    op = DeviceOperator(mf, "XSF", sa=sa, fglobal=fg, foo=0.7, remove=o.re, k_mode="stored")
+    op.set_oo_basis(o.vects)
+    assert rel(op.apply(z), vind(z)) < RTOL

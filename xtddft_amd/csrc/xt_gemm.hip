@@ -99,8 +99,12 @@ __device__ __forceinline__ void swap16_d(double& A, double& B) {
 // TAG only gives hot call sites their own kernel symbol (rocprofv3 identity).
 // MINW = waves per SIMD the register budget must allow (occupancy target).
 // MODE: 0 plain GEMM, 1 / 2 fused XC contractions (XcFuse, xt_internal.h).
+// ROWSIMD: waves w and w + 4 share a SIMD; by default wn = w % WGN, so with WGN = 4
+// the column index picks the SIMD and a ragged last column tile (N % BN small) lands
+// on one SIMD.  ROWSIMD (WGM = 4) takes wm = w % 4 instead: a ragged column edge then
+// spreads over all four SIMDs (a ragged row edge concentrates).
 template <int BM, int BN, int WGM, int WGN, int BK, int MINW, bool A_KC, bool B_KC, int TAG, int MODE = 0,
-          int MAP = 0>
+          int MAP = 0, bool ROWSIMD = false>
 __global__ void __launch_bounds__(64 * WGM * WGN, MINW)
 dgemm_kernel(GemmParams p) {
   static_assert(MODE == 0 || ((BM == 128 || (MODE == 2 && BM == 64)) && WGM * WGN == 8 && !A_KC && B_KC),
@@ -128,7 +132,8 @@ dgemm_kernel(GemmParams p) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);   // wave-uniform (SGPR) copy
-  const int wm = wave_u / WGN, wn = wave_u % WGN;
+  const int wm = ROWSIMD ? wave_u % WGM : wave_u / WGN;
+  const int wn = ROWSIMD ? wave_u / WGM : wave_u % WGN;
   const int q = lane >> 4, r16 = lane & 15;
 
   // ---- block -> (tile, batch, split) ---------------------------------------
@@ -612,13 +617,14 @@ static const Cfg kCfg[] = {   // (bm, bn, bk, concurrent block slots, wgm, wgn)
   {128, 128, 16, 512, 2, 4},   // 5: C8 with BK 16, two blocks per CU
   {256, 128, 16, 256, 4, 2},   // 6: 256x128, 8 waves of 64x64, BK 16 (tuning only)
   {128, 64, 16, 512, 2, 4},    // 7: 128x64, 8 waves of 64x16, BK 16, two blocks per CU
+  {128, 128, 16, 512, 4, 2},   // 8: cfg 5 as 8 waves of 32x64 with rows on the SIMDs (ROWSIMD)
 };
 
 template <int BM, int BN, int WGM, int WGN, int BKT, int MINW, bool AK, bool BKc, int TAG, int MODE = 0,
-          int MAP = 0>
+          int MAP = 0, bool ROWSIMD = false>
 static void launch_one(const GemmParams& p, hipStream_t st) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, BKT, MINW, AK, BKc, TAG, MODE, MAP>),
+  hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, BKT, MINW, AK, BKc, TAG, MODE, MAP, ROWSIMD>),
                      dim3(tiles, 1, p.nbatch * p.nsplit), dim3(64 * WGM * WGN), 0, st, p);
 }
 
@@ -640,17 +646,17 @@ int xc_m_bn() {
 // Tagged call sites get their own kernel symbol for their one operand layout:
 // 1 exchange contraction (A k-contig, B n-contig), 2 XC forward U (k, k),
 // 3 XC back L (m, n), 4 XC forward W (k, n), 5 XC back M (m, n).
-template <int BM, int BN, int WGM, int WGN, int BKT, int MINW>
+template <int BM, int BN, int WGM, int WGN, int BKT, int MINW, bool RS = false>
 static void launch_cfg(const GemmParams& p, hipStream_t st, bool akc, bool bkc, int tag) {
-  if (tag == 1 && akc && !bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, true, false, 1>(p, st);
-  else if (tag == 2 && akc && bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, true, true, 2>(p, st);
-  else if (tag == 3 && !akc && !bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, false, false, 3>(p, st);
-  else if (tag == 4 && akc && !bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, true, false, 4>(p, st);
-  else if (tag == 5 && !akc && !bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, false, false, 5>(p, st);
-  else if (akc && bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, true, true, 0>(p, st);
-  else if (akc)        launch_one<BM, BN, WGM, WGN, BKT, MINW, true, false, 0>(p, st);
-  else if (bkc)        launch_one<BM, BN, WGM, WGN, BKT, MINW, false, true, 0>(p, st);
-  else                 launch_one<BM, BN, WGM, WGN, BKT, MINW, false, false, 0>(p, st);
+  if (tag == 1 && akc && !bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, true, false, 1, 0, 0, RS>(p, st);
+  else if (tag == 2 && akc && bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, true, true, 2, 0, 0, RS>(p, st);
+  else if (tag == 3 && !akc && !bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, false, false, 3, 0, 0, RS>(p, st);
+  else if (tag == 4 && akc && !bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, true, false, 4, 0, 0, RS>(p, st);
+  else if (tag == 5 && !akc && !bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, false, false, 5, 0, 0, RS>(p, st);
+  else if (akc && bkc) launch_one<BM, BN, WGM, WGN, BKT, MINW, true, true, 0, 0, 0, RS>(p, st);
+  else if (akc)        launch_one<BM, BN, WGM, WGN, BKT, MINW, true, false, 0, 0, 0, RS>(p, st);
+  else if (bkc)        launch_one<BM, BN, WGM, WGN, BKT, MINW, false, true, 0, 0, 0, RS>(p, st);
+  else                 launch_one<BM, BN, WGM, WGN, BKT, MINW, false, false, 0, 0, 0, RS>(p, st);
 }
 
 size_t dgemm_workspace_bytes(const GemmDesc& d) {
@@ -675,12 +681,15 @@ static int forced_cfg() {
 // Relative MFMA time of a tile with vm valid rows / vn valid cols: the busiest
 // SIMD's share (waves w and w + 4 share a SIMD; MN-edge waves skip their
 // out-of-range 16x16 sub-tiles), 1 for an interior tile.
+static bool cfg_rowsimd(const Cfg& c) { return &c == &kCfg[8]; }
+
 static double tile_cost(const Cfg& c, int vm, int vn) {
   const int WM = c.bm / c.wgm, WN = c.bn / c.wgn, TM = WM / 16, TN = WN / 16;
   const int nw = c.wgm * c.wgn;
+  const bool rs = cfg_rowsimd(c);
   double simd[4] = {0, 0, 0, 0};
   for (int w = 0; w < nw; ++w) {
-    const int wm = w / c.wgn, wn = w % c.wgn;
+    const int wm = rs ? w % c.wgm : w / c.wgn, wn = rs ? w / c.wgm : w % c.wgn;
     int mi = (vm - wm * WM + 15) / 16, nj = (vn - wn * WN + 15) / 16;
     mi = mi < 0 ? 0 : (mi > TM ? TM : mi);
     nj = nj < 0 ? 0 : (nj > TN ? TN : nj);
@@ -770,6 +779,17 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
   // the stored-exchange stream (skinny M, K = N = O V, HBM-bound): the 8-wave
   // two-blocks-per-CU tile keeps more loads in flight than 64x128 (21.4 -> 20.0 ms)
   if (d.tag == 1 && !ff && d.N >= 96) cfg = 5;
+  static const int rowsimd = env_int("XT_ROWSIMD", 1);
+  if (cfg == 5 && rowsimd && !(d.tag == 1 && !ff)) {
+    // ragged column edge: rows on the SIMDs when that makes the edge tiles cheaper
+    const int vm = d.M - ((d.M + 127) / 128 - 1) * 128, vn = d.N - ((d.N + 127) / 128 - 1) * 128;
+    const long tm = (d.M + 127) / 128, tn = (d.N + 127) / 128;
+    auto total = [&](const Cfg& cc) {
+      return (double)(tm - 1) * (tn - 1) * tile_cost(cc, 128, 128) + (double)(tn - 1) * tile_cost(cc, vm, 128) +
+             (double)(tm - 1) * tile_cost(cc, 128, vn) + tile_cost(cc, vm, vn);
+    };
+    if (total(kCfg[8]) < 0.99 * total(kCfg[5])) cfg = 8;
+  }
   if (forced_cfg() >= 0) cfg = forced_cfg();
   const Cfg& c = kCfg[cfg];
   const long units = (long)p.R * ((d.K + c.bk - 1) / c.bk);
@@ -836,6 +856,7 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
     case 5: launch_cfg<128, 128, 2, 4, 16, 4>(p, st, akc, bkc, d.tag); break;
     case 6: launch_cfg<256, 128, 4, 2, 16, 2>(p, st, akc, bkc, d.tag); break;
     case 7: launch_cfg<128, 64, 2, 4, 16, 4>(p, st, akc, bkc, d.tag); break;
+    case 8: launch_cfg<128, 128, 4, 2, 16, 4, true>(p, st, akc, bkc, d.tag); break;
     default: launch_cfg<64, 64, 2, 2, 32, 2>(p, st, akc, bkc, d.tag); break;
   }
   if (p.nsplit > 1) {
