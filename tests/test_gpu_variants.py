@@ -4,8 +4,8 @@ the row counts that take its 160-row streaming tile and its batching.
 
 * XT_M_KERNEL=0  -> XC M-backward through the generic engine's mode 2
   (default: the dedicated kernel, xt_xcm.hip)
-* XT_W_KERNEL=1  -> XC rho-forward through the dedicated kernel (xt_xcw.hip)
-  (default: the engine's mode 1)
+* XT_W_KERNEL=0  -> XC rho-forward through the generic engine's mode 1
+  (default: the dedicated kernel, xt_xcw.hip)
 * XT_XSF_FUSED=0 -> XSF Delta-A exchange as direct DF sandwiches
   (default with the stored exchange: one Kx stream for main + Delta-A exchange)
 Tolerance: 1e-12 relative max-norm on sigma (FP64 round-off of a different
@@ -44,7 +44,8 @@ def env():
             os.environ[k] = v
 
 
-@pytest.mark.parametrize("knobs", [dict(XT_M_KERNEL=0), dict(XT_W_KERNEL=1), dict(XT_M_KERNEL=0, XT_W_KERNEL=1)])
+@pytest.mark.parametrize("knobs", [dict(XT_M_KERNEL=0), dict(XT_W_KERNEL=0), dict(XT_M_KERNEL=0, XT_W_KERNEL=0),
+                                   dict(XT_M_KERNEL=1, XT_W_KERNEL=1)])
 @pytest.mark.parametrize("nc,no,nao", [(5, 2, 26), (33, 1, 60), (95, 2, 130), (120, 3, 150)])
 def test_xc_kernel_variants(hiplib, env, knobs, nc, no, nao):
     """O = 7, 34, 97 and 123: one to eight 16-row sub-tiles of the dedicated kernels."""

@@ -96,7 +96,7 @@ struct xt_ctx {
   int win_p0 = 0, win_np = -1;   // -1: all aux rows
   bool skinny = true;            // stored exchange through the skinny streaming kernel (XT_SKINNY=0: generic tile)
   bool m_kernel = true;          // XC M-backward through xt_xcm.hip (XT_M_KERNEL=0: the engine's mode 2)
-  bool w_kernel = false;         // XC rho-forward through xt_xcw.hip (XT_W_KERNEL=1; default: the engine's mode 1)
+  bool w_kernel = true;          // XC rho-forward through xt_xcw.hip (XT_W_KERNEL=0: the engine's mode 1)
   bool xsf_fused = true;         // XSF Delta-A exchange through the stored matrix (XT_XSF_FUSED=0: direct)
   int kr0 = 0, kr1 = -1;         // -1: all O rows
 };
@@ -241,7 +241,7 @@ int xt_create(const xt_desc* desc, xt_ctx** out) {
     const char* em = getenv("XT_M_KERNEL");
     c->m_kernel = !(em && atoi(em) == 0);
     const char* ew = getenv("XT_W_KERNEL");
-    c->w_kernel = ew && atoi(ew) == 1;
+    c->w_kernel = !(ew && atoi(ew) == 0);
     const char* ex = getenv("XT_XSF_FUSED");
     c->xsf_fused = !(ex && atoi(ex) == 0);
   }

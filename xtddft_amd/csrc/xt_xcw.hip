@@ -22,6 +22,7 @@
 // the fragment / weight reads (16 consecutive g, two rows of opposite parity per
 // 32-lane group) land in opposite bank halves.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include "xt_internal.h"
 
 namespace xt {
@@ -32,7 +33,10 @@ typedef double d4w __attribute__((ext_vector_type(4)));
 constexpr int WA = 32;           // virtuals per a-tile (2 MFMA row sub-tiles)
 constexpr int TMA = WA / 16;
 constexpr int WXB = 8;           // trial pairs per block (one per wave)
-constexpr int ZD = 2;            // Zp prefetch ring depth (k-steps; divides KS = KI / 4)
+#ifndef XCW_ZD
+#define XCW_ZD 4
+#endif
+constexpr int ZD = XCW_ZD;       // Zp prefetch ring depth (k-steps)
 
 __device__ __forceinline__ int swz(int row) { return (row & 15) | ((row & 1) << 4); }
 
@@ -115,12 +119,14 @@ k_xc_rho_w(int O, int nx, int V, int n,
   // columns at WA + 16 t + r16 (past V: the next pair's values, weighted by zero)
   const double* zb = Z + (long)(wave_on ? xg : 0) * zx + r16 + (long)q * zi;
   double zq[ZD][TMA];
-  int zu_at = 0, zu_s = 0;                     // next k-step to load
+  const long zstep = 4 * zi;
+  const double* zn = zb;                       // next k-step to load: a-tile za, k-step zs
+  int zs = 0, za = 0;
   auto load_z = [&](int slot) XT_INLINE {
-    const double* p = zb + (long)(4 * zu_s) * zi + zu_at * WA;
 #pragma unroll
-    for (int t = 0; t < TMA; ++t) zq[slot][t] = p[16 * t];
-    if (++zu_s == KS) { zu_s = 0; zu_at = zu_at + 1 < nat ? zu_at + 1 : zu_at; }
+    for (int t = 0; t < TMA; ++t) zq[slot][t] = zn[16 * t];
+    if (++zs == KS) { zs = 0; za = za + 1 < nat ? za + 1 : za; zn = zb + za * WA; }
+    else zn += zstep;
   };
 #pragma unroll
   for (int d = 0; d < ZD; ++d) load_z(d);
@@ -133,6 +139,36 @@ k_xc_rho_w(int O, int nx, int V, int n,
     for (int c = 0; c < 3; ++c) racc[j][c] = 0.0;
 
   const int p_lane = q * GB;                   // B image: row 4 s + q, column (16 j + r16) ^ swz
+  // one k-step from ring slot `slot` (a compile-time constant after unrolling)
+  auto step = [&](int s, int slot) XT_INLINE {
+    const int i = 4 * s + q;
+    const int sw = swz(i);
+    double bf[TNG];
+#pragma unroll
+    for (int j = 0; j < TNG; ++j) bf[j] = sP[p_lane + 4 * s * GB + ((16 * j + r16) ^ sw)];
+    double af[TMA];
+#pragma unroll
+    for (int t = 0; t < TMA; ++t) af[t] = zq[slot][t];
+    load_z(slot);
+#pragma unroll
+    for (int t = 0; t < TMA; ++t)
+#pragma unroll
+      for (int j = 0; j < TNG; ++j)
+        acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t], bf[j], acc[t][j], 0, 0, 0);
+  };
+  // the K loop of one a-tile whose first k-step sits in ring slot PH (KS is even, so
+  // PH is even); the slots stay compile-time constants inside each unrolled group
+  auto kloop = [&](auto PH) XT_INLINE {
+    constexpr int P = decltype(PH)::value;
+    int s = 0;
+    for (; s + ZD <= KS; s += ZD) {
+#pragma unroll
+      for (int d = 0; d < ZD; ++d) step(s + d, (P + d) % ZD);
+    }
+#pragma unroll
+    for (int d = 0; d < ZD; ++d)
+      if (s + d < KS) step(s + d, (P + d) % ZD);
+  };
   __syncthreads();
   for (int at = 0; at < nat; ++at) {
     const int buf = at & 1;
@@ -142,25 +178,16 @@ k_xc_rho_w(int O, int nx, int V, int n,
 #pragma unroll
       for (int j = 0; j < TNG; ++j) acc[t][j] = (d4w){0.0, 0.0, 0.0, 0.0};
     if (wave_on) {
-      // K loop over the occupied rows, ZD k-steps per unrolled body (static ring slots)
-      for (int s0 = 0; s0 < KS; s0 += ZD) {
-#pragma unroll
-        for (int d = 0; d < ZD; ++d) {
-          const int s = s0 + d;
-          const int i = 4 * s + q;
-          const int sw = swz(i);
-          double bf[TNG];
-#pragma unroll
-          for (int j = 0; j < TNG; ++j) bf[j] = sP[p_lane + 4 * s * GB + ((16 * j + r16) ^ sw)];
-          double af[TMA];
-#pragma unroll
-          for (int t = 0; t < TMA; ++t) af[t] = zq[d][t];
-          load_z(d);
-#pragma unroll
-          for (int t = 0; t < TMA; ++t)
-#pragma unroll
-            for (int j = 0; j < TNG; ++j)
-              acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t], bf[j], acc[t][j], 0, 0, 0);
+      const int ph = (int)(((long)at * KS) % ZD);
+      if constexpr (ZD == 4) {
+        if (ph == 0) kloop(std::integral_constant<int, 0>{});
+        else         kloop(std::integral_constant<int, 2>{});
+      } else {
+        switch (ph) {
+          case 0: kloop(std::integral_constant<int, 0>{}); break;
+          case 2: kloop(std::integral_constant<int, 2 % ZD>{}); break;
+          case 4: kloop(std::integral_constant<int, 4 % ZD>{}); break;
+          default: kloop(std::integral_constant<int, 6 % ZD>{}); break;
         }
       }
       // contraction with the a-tile's weights: acc[t][j][r] = T[a = 16 t + q + 4 r][g = 16 j + r16]
