@@ -28,6 +28,10 @@ def tag_of(name, stored=False):
     exchange class."""
     if "k_skinny" in name:
         return "mo_exchange_stored"
+    if "k_xc_rho_w" in name:
+        return "xc_forward_w"
+    if "k_xc_back_m" in name:          # the dedicated kernel and its split reduce
+        return "xc_back_m"
     if "dgemm_kernel<" not in name:
         return None
     t = int(name.split("dgemm_kernel<")[1].split(">")[0].split(",")[8])
@@ -38,7 +42,8 @@ def tag_of(name, stored=False):
 
 def is_aux(name):
     """helper launches of a class (counted in its bytes and time, not its launches)"""
-    return "k_skinny_reduce" in name or "k_skinny_transpose" in name
+    return ("k_skinny_reduce" in name or "k_skinny_transpose" in name or "k_xc_back_m_reduce" in name
+            or "k_xsf_split4" in name or "k_xsf_combine4" in name)
 
 
 def short(name):

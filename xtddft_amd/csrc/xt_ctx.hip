@@ -96,7 +96,7 @@ struct xt_ctx {
   int win_p0 = 0, win_np = -1;   // -1: all aux rows
   bool skinny = true;            // stored exchange through the skinny streaming kernel (XT_SKINNY=0: generic tile)
   bool m_kernel = true;          // XC M-backward through xt_xcm.hip (XT_M_KERNEL=0: the engine's mode 2)
-  bool w_kernel = true;          // XC rho-forward through xt_xcw.hip (XT_W_KERNEL=0: the engine's mode 1)
+  int w_kernel = 2;              // XC rho-forward: 1 xt_xcw.hip, 0 the engine's mode 1, 2 by size (XT_W_KERNEL)
   bool xsf_fused = true;         // XSF Delta-A exchange through the stored matrix (XT_XSF_FUSED=0: direct)
   int kr0 = 0, kr1 = -1;         // -1: all O rows
 };
@@ -241,7 +241,7 @@ int xt_create(const xt_desc* desc, xt_ctx** out) {
     const char* em = getenv("XT_M_KERNEL");
     c->m_kernel = !(em && atoi(em) == 0);
     const char* ew = getenv("XT_W_KERNEL");
-    c->w_kernel = !(ew && atoi(ew) == 0);
+    c->w_kernel = ew ? (atoi(ew) == 0 ? 0 : 1) : 2;
     const char* ex = getenv("XT_XSF_FUSED");
     c->xsf_fused = !(ex && atoi(ex) == 0);
   }
@@ -993,7 +993,10 @@ static int xc_response(xt_ctx* c, int nz) {
       f1.C = Ug[q]; f1.ldc = ldU[q];
       f1.tag = 2;
       RET(gemm(c, f1));
-      if (gga && c->w_kernel && xc_rho_w_lds_bytes(O) <= 160 * 1024) {
+      // the dedicated kernel pays off from ~6 occupied 16-row blocks up (O = 101: 168.6 vs
+      // 173.1 ms/step; O = 34 / 37: 18 % / 15 % slower than the engine's mode 1)
+      const bool w_ded = c->w_kernel == 1 || (c->w_kernel == 2 && O >= 96);
+      if (gga && w_ded && xc_rho_w_lds_bytes(O) <= 160 * 1024) {
         // dedicated kernel (xt_xcw.hip); tag 4 timing
         bool prof = false;
         RET(prof_begin(c, 4, 2.0 * nzg * V * (double)n * O,
