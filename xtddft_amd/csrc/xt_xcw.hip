@@ -122,11 +122,20 @@ k_xc_rho_w(int O, int nx, int V, int n,
   const long zstep = 4 * zi;
   const double* zn = zb;                       // next k-step to load: a-tile za, k-step zs
   int zs = 0, za = 0;
+  // branch-free advance (a branch here splits the unrolled K loop into one basic
+  // block per k-step and the compiler then stops prefetching LDS reads across steps):
+  // past the a-tile's last k-step the pointer jumps to the next tile's first row
+  // (the last tile repeats itself: those loads are never consumed)
+  const long zwrap = (long)WA - (long)KS * zstep;
   auto load_z = [&](int slot) XT_INLINE {
 #pragma unroll
     for (int t = 0; t < TMA; ++t) zq[slot][t] = zn[16 * t];
-    if (++zs == KS) { zs = 0; za = za + 1 < nat ? za + 1 : za; zn = zb + za * WA; }
-    else zn += zstep;
+    ++zs;
+    const bool wrap = zs == KS;
+    const bool last = za + 1 >= nat;
+    zs = wrap ? 0 : zs;
+    za = wrap ? za + 1 : za;
+    zn += zstep + (wrap ? (last ? -(long)KS * zstep : zwrap) : 0L);
   };
 #pragma unroll
   for (int d = 0; d < ZD; ++d) load_z(d);
