@@ -806,8 +806,9 @@ static int build_kx(xt_ctx* c) {
   Group gr[2];
   const int ngr = channel_groups(c, gr);
   if (blk == 0) { c->kx_valid = true; return 0; }
-  RET(c->Kx.ensure(blk * ngr));
-  HIPCHK(hipMemsetAsync(c->Kx.p, 0, blk * ngr * 8, c->st));
+  // + zeroed slack rows after the last group (the streaming kernel's tail loads)
+  RET(c->Kx.ensure(blk * ngr + (size_t)SKINNY_B_SLACK * ld));
+  HIPCHK(hipMemsetAsync(c->Kx.p, 0, c->Kx.n * 8, c->st));
   for (int q = 0; q < ngr; ++q) {
     double* K = c->Kx.p + (size_t)q * blk - (size_t)i0 * V * ld;   // row (i,a) at (i V + a) ld
     for (int pass = 0; pass < 2; ++pass) {

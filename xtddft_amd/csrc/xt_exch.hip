@@ -79,8 +79,8 @@ k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
     for (int e = 0; e < A_E; ++e) {
       const int piece = tid + 512 * e;
       const int kk = piece / (SK_MP / 2), mm = 2 * (piece % (SK_MP / 2));
-      const int k = k0 + ch * SK_BK + kk;
-      const d2x v = *(const d2x*)(AT + (long)(k < K ? k : K - 1) * SK_MP + mm);
+      const int k = k0 + ch * SK_BK + kk;   // <= K + SK_BK - 1: AT's zeroed slack rows
+      const d2x v = *(const d2x*)(AT + (long)k * SK_MP + mm);
       ra[e] = k < k1 ? v : (d2x){0.0, 0.0};
     }
   };
@@ -94,9 +94,14 @@ k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
   // B: k-step s of this split -> row k0 + 4 s + q, clamped to K - 1 (those rows
   // meet zero A rows); branch-free so the loads pipeline across k-steps
   typedef double bvec __attribute__((ext_vector_type(SK_TN)));
+  // running row pointer (no per-load clamp / 64-bit multiply): rows past K are the
+  // caller's zeroed slack (SKINNY_B_SLACK rows), met by zero A rows
+  const double* bp = B + (long)(k0 + q) * ldb + cl;
+  const long bstep = 4 * ldb;
   auto load_b = [&](int s, bvec& v) XT_INLINE {
-    const int k = k0 + 4 * s + q;
-    const double* p = B + (long)(k < K ? k : K - 1) * ldb + cl;
+    (void)s;
+    const double* p = bp;
+    bp += bstep;
     if constexpr (SK_TN == 4) {
       const d2x lo = *(const d2x*)p, hi = *(const d2x*)(p + 2);
       v = (bvec){lo[0], lo[1], hi[0], hi[1]};
@@ -173,13 +178,14 @@ __global__ void k_skinny_reduce(int M, int N, int nsplit, int MP, const double* 
   }
 }
 
-// A (M x K, row stride lda) -> AT (K x MP), zero-padded rows m >= M
-__global__ void k_skinny_transpose(int M, int K, int MP, const double* __restrict__ A, long lda,
+// A (M x K, row stride lda) -> AT (K x MP), zero-padded rows m >= M, and kslack
+// zero rows past K
+__global__ void k_skinny_transpose(int M, int K, int kslack, int MP, const double* __restrict__ A, long lda,
                                    double* __restrict__ AT) {
-  const long total = (long)K * MP;
+  const long total = (long)(K + kslack) * MP;
   for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
     const int k = (int)(t / MP), m = (int)(t % MP);
-    AT[t] = m < M ? A[(long)m * lda + k] : 0.0;
+    AT[t] = (m < M && k < K) ? A[(long)m * lda + k] : 0.0;
   }
 }
 
@@ -206,7 +212,7 @@ int skinny_splits(int N, int K) { return skinny_splits_m(48, N, K); }
 size_t skinny_workspace_bytes(int M, int N, int K) {
   const SkShape sh = sk_shape(M);
   const int nsplit = skinny_splits_m(M, N, K);
-  return sizeof(double) * ((size_t)K * sh.mp + (size_t)nsplit * sh.mp * N);
+  return sizeof(double) * ((size_t)(K + sh.bk) * sh.mp + (size_t)nsplit * sh.mp * N);
 }
 
 int skinny_gemm(int M, int N, int K, double alpha, const double* A, long lda, const double* B, long ldb,
@@ -222,10 +228,10 @@ int skinny_gemm(int M, int N, int K, double alpha, const double* A, long lda, co
   int kchunk = (K + nsplit - 1) / nsplit;
   kchunk = ((kchunk + sh.bk - 1) / sh.bk) * sh.bk;
   double* AT = ws;
-  double* part = ws + (size_t)K * sh.mp;
-  const long tot = (long)K * sh.mp;
+  double* part = ws + (size_t)(K + sh.bk) * sh.mp;
+  const long tot = (long)(K + sh.bk) * sh.mp;
   hipLaunchKernelGGL(k_skinny_transpose, dim3((unsigned)((tot + 255) / 256 < 65536 ? (tot + 255) / 256 : 65536)),
-                     dim3(256), 0, st, M, K, sh.mp, A, lda, AT);
+                     dim3(256), 0, st, M, K, sh.bk, sh.mp, A, lda, AT);
   const int strips = (N + sh.bn - 1) / sh.bn;
   const int used = (K + kchunk - 1) / kchunk;
   if (sh.mp == 48)

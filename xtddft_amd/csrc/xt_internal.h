@@ -69,6 +69,9 @@ void plan_gemm(const GemmDesc& d, GemmParams* p, int* cfg);
 // B (K x N, 16-B aligned rows of stride ldb: a multiple of 4 >= N, the padding
 // readable) streamed once from HBM
 constexpr int SKINNY_MAX_M = 160;   // 48-row tile up to 48 rows, 160-row tile beyond
+// B must stay readable (finite, zero-filled) SKINNY_B_SLACK rows past row K - 1: the
+// streaming loads run a whole chunk plus the prefetch ring past a split's end
+constexpr int SKINNY_B_SLACK = 128;
 int skinny_splits(int N, int K);
 size_t skinny_workspace_bytes(int M, int N, int K);
 int skinny_gemm(int M, int N, int K, double alpha, const double* A, long lda, const double* B, long ldb,

@@ -22,6 +22,7 @@
 // the fragment / weight reads (16 consecutive g, two rows of opposite parity per
 // 32-lane group) land in opposite bank halves.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <type_traits>
 #include "xt_internal.h"
 
@@ -53,7 +54,7 @@ __device__ __forceinline__ double rows4(double v) {
   return pair(pair(v, false), true);
 }
 
-template <int TNG>
+template <int TNG, bool BRANCHY>
 __global__ void __launch_bounds__(512, 1)
 k_xc_rho_w(int O, int nx, int V, int n,
            const double* __restrict__ PO, long ldp,
@@ -122,20 +123,26 @@ k_xc_rho_w(int O, int nx, int V, int n,
   const long zstep = 4 * zi;
   const double* zn = zb;                       // next k-step to load: a-tile za, k-step zs
   int zs = 0, za = 0;
-  // branch-free advance (a branch here splits the unrolled K loop into one basic
-  // block per k-step and the compiler then stops prefetching LDS reads across steps):
-  // past the a-tile's last k-step the pointer jumps to the next tile's first row
-  // (the last tile repeats itself: those loads are never consumed)
+  // advance to the next k-step; past the a-tile's last k-step the pointer jumps to the
+  // next tile's first row (the last tile repeats itself: those loads are never
+  // consumed).  BRANCHY (default): an if/else, which splits the unrolled K loop into
+  // one basic block per k-step; the select-based form keeps one block per 4 k-steps
+  // but measured 4 % slower.
   const long zwrap = (long)WA - (long)KS * zstep;
   auto load_z = [&](int slot) XT_INLINE {
 #pragma unroll
     for (int t = 0; t < TMA; ++t) zq[slot][t] = zn[16 * t];
-    ++zs;
-    const bool wrap = zs == KS;
-    const bool last = za + 1 >= nat;
-    zs = wrap ? 0 : zs;
-    za = wrap ? za + 1 : za;
-    zn += zstep + (wrap ? (last ? -(long)KS * zstep : zwrap) : 0L);
+    if constexpr (BRANCHY) {
+      if (++zs == KS) { zs = 0; za = za + 1 < nat ? za + 1 : za; zn = zb + za * WA; }
+      else zn += zstep;
+    } else {
+      ++zs;
+      const bool wrap = zs == KS;
+      const bool last = za + 1 >= nat;
+      zs = wrap ? 0 : zs;
+      za = wrap ? za + 1 : za;
+      zn += zstep + (wrap ? (last ? -(long)KS * zstep : zwrap) : 0L);
+    }
   };
 #pragma unroll
   for (int d = 0; d < ZD; ++d) load_z(d);
@@ -246,16 +253,25 @@ int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const doub
   if (O <= 0 || nx <= 0 || V <= 0 || n <= 0) return 0;
   const size_t lds = xc_rho_w_lds_bytes(O);
   if (lds > 160 * 1024) return XT_ERR_ARG;
+  // XT_W_RING=0: the select-based (branch-free) ring advance; measured slower on the
+  // same box (178.2 vs 170.6 ms/step; engine mode 1: 173.4)
+  static const int branchy = [] { const char* e = getenv("XT_W_RING"); return e ? atoi(e) : 1; }();
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_xc_rho_w<kWTng>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_xc_rho_w<kWTng, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_xc_rho_w<kWTng, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr = true;
   }
   const int GB = 16 * kWTng;
   const int blocks = ((n + GB - 1) / GB) * ((nx + WXB - 1) / WXB);
-  hipLaunchKernelGGL(k_xc_rho_w<kWTng>, dim3(blocks), dim3(512), lds, st, O, nx, V, n, PO, ldp, Z, zi, zx, W,
-                     wc, wg, R, rg);
+  if (branchy)
+    hipLaunchKernelGGL((k_xc_rho_w<kWTng, true>), dim3(blocks), dim3(512), lds, st, O, nx, V, n, PO, ldp, Z, zi, zx,
+                       W, wc, wg, R, rg);
+  else
+    hipLaunchKernelGGL((k_xc_rho_w<kWTng, false>), dim3(blocks), dim3(512), lds, st, O, nx, V, n, PO, ldp, Z, zi,
+                       zx, W, wc, wg, R, rg);
   return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
 }
 
