@@ -465,21 +465,42 @@ k_xc_point(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
   }
   double* Ub[2] = {U0 + g * ldU0, U1 + g * ldU1};
   double* Rb[2] = {R0 ? R0 + g * ldR0 : nullptr, R1 ? R1 + g * ldR1 : nullptr};
-  for (int x = 0; x < nz; ++x) {
-    double v[NV];
+  // the next x's U row and rhoW values are loaded before this x's reductions, so
+  // two rows per wave are in flight (the loop is HBM-latency-bound otherwise)
+  double un[2][IC], rn[2][NC > 1 ? NC - 1 : 1];
+  auto load_x = [&](int x) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      double u[IC];
 #pragma unroll
       for (int m = 0; m < IC; ++m) {
         const int i = lane + 64 * m;
-        u[m] = i < O ? Ub[s][(long)x * O + i] : 0.0;
+        un[s][m] = i < O ? Ub[s][(long)x * O + i] : 0.0;
       }
+      if constexpr (NC > 1) {
+#pragma unroll
+        for (int c = 1; c < NC; ++c) rn[s][c - 1] = Rb[s][3 * x + c - 1];
+      }
+    }
+  };
+  load_x(0);
+  for (int x = 0; x < nz; ++x) {
+    double u[2][IC], rw_[2][NC > 1 ? NC - 1 : 1];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int m = 0; m < IC; ++m) u[s][m] = un[s][m];
+#pragma unroll
+      for (int c = 0; c < (NC > 1 ? NC - 1 : 1); ++c) rw_[s][c] = rn[s][c];
+    }
+    if (x + 1 < nz) load_x(x + 1);
+    double v[NV];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         double a = 0.0;
 #pragma unroll
-        for (int m = 0; m < IC; ++m) a += u[m] * ph[s][c][m];
+        for (int m = 0; m < IC; ++m) a += u[s][m] * ph[s][c][m];
         v[s * NC + c] = a;
       }
     }
@@ -491,7 +512,7 @@ k_xc_point(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int c = 1; c < NC; ++c) rho[s * NC + c] += Rb[s][3 * x + c - 1];
+        for (int c = 1; c < NC; ++c) rho[s * NC + c] += rw_[s][c - 1];
     }
     double wl = 0.0;
 #pragma unroll
