@@ -51,7 +51,24 @@ struct BmLds {
   static constexpr int BUF = A + W + R;
 };
 
-template <int TM, bool GEN_FIRST>
+// rows4: sum of v over the four 16-lane rows (lanes l, l^16, l^32, l^48), in every lane
+__device__ __forceinline__ double rows4_m(double v) {
+  auto pair = [](double x, bool p32) XT_INLINE {
+    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+    const auto a = p32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                       : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = p32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                       : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+  };
+  return pair(pair(v, false), true);
+}
+
+// RV > 0: the last 16-row block of the occupied rows holds only RV <= 8 rows (O = 16
+// (TM - 1) + RV); those rows are accumulated on the VALU (RV x 2 FMAs per k-step
+// against the same B fragments, ~55 cycles at RV = 5) instead of a 16-row MFMA
+// sub-tile (2 MFMAs, ~145 cycles), and reduced over the four k-rows once per block.
+template <int TM, bool GEN_FIRST, int RV = 0>
 __global__ void __launch_bounds__(512, 1)
 k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
             const double* __restrict__ PO, long ldp,
@@ -156,11 +173,16 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
     }
   };
 
-  d4m acc[TM][2];
+  constexpr int TMM = RV ? TM - 1 : TM;        // MFMA row sub-tiles
+  constexpr int RVA = RV ? RV : 1;
+  d4m acc[TMM > 0 ? TMM : 1][2];
 #pragma unroll
-  for (int t = 0; t < TM; ++t)
+  for (int t = 0; t < TMM; ++t)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[t][j] = (d4m){0.0, 0.0, 0.0, 0.0};
+  double part[RVA][2];
+#pragma unroll
+  for (int r = 0; r < RVA; ++r) part[r][0] = part[r][1] = 0.0;
 
   // one K-tile: 8 k-steps; lane (q, r16) feeds k = g_l = 4 s + q.  Row parity of g_l
   // is the parity of q, so the swizzles are per-lane constants and every LDS address
@@ -185,15 +207,26 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
       }
     };
     auto mma = [&](int ks, const double* b) XT_INLINE {
-      double af[TM];
+      double af[TMM > 0 ? TMM : 1];
 #pragma unroll
-      for (int t = 0; t < TM; ++t) {
+      for (int t = 0; t < TMM; ++t) {
         // (16 t + r16) ^ sw = 16 (t ^ (sw / 16)) + r16: the swizzle permutes whole sub-tiles
         const int tt = SWA ? (t ^ (q & 1)) : t;
         af[t] = s[q * PA + 4 * ks * PA + 16 * tt + r16];
       }
+      if constexpr (RV > 0) {
+        // the remainder rows: phi_i(g) for i = 16 (TM - 1) + r, broadcast over the 16 lanes of a k-row
+        const int tl = SWA ? ((TM - 1) ^ (q & 1)) : TM - 1;
+        const double* rrw = s + q * PA + 4 * ks * PA + 16 * tl;
 #pragma unroll
-      for (int t = 0; t < TM; ++t)
+        for (int r = 0; r < RV; ++r) {
+          const double v = rrw[r];
+          part[r][0] += v * b[0];
+          part[r][1] += v * b[1];
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < TMM; ++t)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t], b[j], acc[t][j], 0, 0, 0);
@@ -236,7 +269,7 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
   // C/D layout: col = lane & 15, row = q + 4 reg
   double* o = out + (long)split * slab;
 #pragma unroll
-  for (int t = 0; t < TM; ++t)
+  for (int t = 0; t < TMM; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = 16 * t + q + 4 * r;
@@ -247,6 +280,16 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
         if (a < V) o[(long)i * ldo + (long)xg * V + a] = acc[t][j][r];
       }
     }
+  if constexpr (RV > 0) {
+#pragma unroll
+    for (int r = 0; r < RV; ++r)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const double v = rows4_m(part[r][j]);
+        const int i = 16 * (TM - 1) + r, a = a0 + 16 * j + r16;
+        if (q == 0 && i < O && a < V) o[(long)i * ldo + (long)xg * V + a] = v;
+      }
+  }
 }
 
 // accT[i][col] += sum_s ws[s][i][col]   (fixed order)
@@ -283,10 +326,35 @@ size_t xc_back_m_workspace_bytes(int O, int nx, int V, int n) {
   return sizeof(double) * (size_t)s * O * (size_t)nx * V;
 }
 
+template <int TM, int RV>
+static void launch_back_m_rv(int O, int nx, int V, int n, int kps, int blocks, const double* PO, long ldp,
+                             const double* W, long wc, long wg, const double* R, long rg, double* ws, long slab,
+                             hipStream_t st) {
+  hipLaunchKernelGGL((k_xc_back_m<TM, false, RV>), dim3(blocks), dim3(512), 0, st, O, nx, V, n, kps, PO, ldp, W, wc,
+                     wg, R, rg, ws, (long)nx * V, slab);
+}
+
+// remainder rows on the VALU for the occupied counts of the BASELINE shapes
+// (O = 33..40: C2, C5; O = 97..104: the headline); XT_M_RV=0 keeps 16-row MFMA tiles
+template <int TM>
+static bool launch_back_m_valu(int O, int nx, int V, int n, int kps, int blocks, const double* PO, long ldp,
+                               const double* W, long wc, long wg, const double* R, long rg, double* ws, long slab,
+                               hipStream_t st) {
+  const int rv = O - 16 * (TM - 1);
+  if (TM == 7 && rv > 6) return false;                 // (spills at 256 VGPRs)
+#define XT_RV(N) case N: launch_back_m_rv<TM, N>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); return true;
+  switch (rv) { XT_RV(1) XT_RV(2) XT_RV(3) XT_RV(4) XT_RV(5) XT_RV(6) XT_RV(7) XT_RV(8) default: return false; }
+#undef XT_RV
+}
+
 template <int TM>
 static void launch_back_m(int O, int nx, int V, int n, int kps, int blocks, const double* PO, long ldp,
                           const double* W, long wc, long wg, const double* R, long rg, double* ws, long slab,
                           hipStream_t st) {
+  static const int rv_on = [] { const char* e = getenv("XT_M_RV"); return e ? atoi(e) : 1; }();
+  if constexpr (TM == 3 || TM == 7) {
+    if (rv_on && launch_back_m_valu<TM>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st)) return;
+  }
   static const int gen_first = [] { const char* e = getenv("XT_M_GEN"); return e ? atoi(e) : 0; }();
   if (gen_first)
     hipLaunchKernelGGL((k_xc_back_m<TM, true>), dim3(blocks), dim3(512), 0, st, O, nx, V, n, kps, PO, ldp, W, wc, wg,

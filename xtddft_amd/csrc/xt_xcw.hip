@@ -255,7 +255,8 @@ int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const doub
   if (lds > 160 * 1024) return XT_ERR_ARG;
   // XT_W_RING=0: the select-based (branch-free) ring advance; measured slower on the
   // same box (178.2 vs 170.6 ms/step; engine mode 1: 173.4)
-  static const int branchy = [] { const char* e = getenv("XT_W_RING"); return e ? atoi(e) : 1; }();
+  const char* ering = getenv("XT_W_RING");    // read per call: tests switch it in-process
+  const int branchy = ering ? atoi(ering) : 1;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)k_xc_rho_w<kWTng, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
