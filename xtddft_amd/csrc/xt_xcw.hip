@@ -206,24 +206,37 @@ k_xc_rho_w(int O, int nx, int V, int n,
           default: kloop(std::integral_constant<int, 6 % ZD>{}); break;
         }
       }
-      // contraction with the a-tile's weights: acc[t][j][r] = T[a = 16 t + q + 4 r][g = 16 j + r16]
+      // contraction with the a-tile's weights: acc[t][j][r] = T[a = 16 t + q + 4 r][g = 16 j + r16].
+      // Half a row (t, r) of weights at a time, the next half's reads issued before this
+      // half's FMAs (two 6-value buffers; unfenced, the compiler hoists all 96 reads and
+      // spills; fenced without the lookahead, every row waits out the LDS latency)
       const double* w = sW + buf * W_IMG;
+      constexpr int JH = TNG / 2;                // half a row: JH column sub-tiles x 3 weights
+      double wb[2][JH * 3];
+      auto wread = [&](int h, double* dst) XT_INLINE {
+        const int rw = h / 2, j0 = (h % 2) * JH;
+        const int t = rw / 4, r = rw % 4;
+        const int a = 16 * t + q + 4 * r;
+        const int sa = swz(a);
 #pragma unroll
-      for (int t = 0; t < TMA; ++t)
+        for (int jj = 0; jj < JH; ++jj) {
+          const int col = (16 * (j0 + jj) + r16) ^ sa;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int a = 16 * t + q + 4 * r;
-          const int sa = swz(a);
-#pragma unroll
-          for (int j = 0; j < TNG; ++j) {
-            const int col = (16 * j + r16) ^ sa;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) racc[j][c] += acc[t][j][r] * w[(c * WA + a) * GB + col];
-          }
-          // one row at a time: unfenced, the compiler hoists all 96 weight reads
-          // ahead of the FMAs and spills
-          __builtin_amdgcn_sched_barrier(0);
+          for (int c = 0; c < 3; ++c) dst[3 * jj + c] = w[(c * WA + a) * GB + col];
         }
+      };
+      wread(0, wb[0]);
+#pragma unroll
+      for (int h = 0; h < 8 * TMA; ++h) {
+        if (h + 1 < 8 * TMA) wread(h + 1, wb[(h + 1) & 1]);
+        const int rw = h / 2, j0 = (h % 2) * JH;
+        const int t = rw / 4, r = rw % 4;
+#pragma unroll
+        for (int jj = 0; jj < JH; ++jj)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) racc[j0 + jj][c] += acc[t][j0 + jj][r] * wb[h & 1][3 * jj + c];
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     if (at + 1 < nat) store_w(buf ^ 1, at + 1);
