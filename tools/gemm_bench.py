@@ -12,13 +12,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from xtddft_amd import _capi, build  # noqa: E402
 
 SHAPES = [
-    ("exch_step2  (k,n)", 4040, 901, 102 * 901, 0, 0),
-    ("xc_fwd_u    (k,k)", 13900, 4040, 901, 0, 1),
-    ("xc_fwd_w    (k,n)", 13900, 36040, 101, 0, 0),
-    ("xc_back_l   (m,n)", 4040, 901, 13900, 1, 0),
-    ("xc_back_m   (m,n)", 101, 36040, 13900, 1, 0),
-    ("exch_step1  (k,n)x64", 101, 36040, 101, 0, 0),
+    ("xc_fwd_u    (k,k)", 65536, 4040, 901, 0, 1),
+    ("xc_back_l   (m,n)", 4040, 901, 65536, 1, 0),
     ("square4096  (k,n)", 4096, 4096, 4096, 0, 0),
+    ("square8192  (k,n)", 8192, 8192, 8192, 0, 0),
 ]
 
 
