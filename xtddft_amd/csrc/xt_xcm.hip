@@ -34,20 +34,23 @@ namespace xt {
 #define XT_INLINE __attribute__((always_inline))
 typedef double d4m __attribute__((ext_vector_type(4)));
 
-constexpr int BM_BK = 32;        // grid points per K-tile
 constexpr int BM_AB = 32;        // virtuals per block (2 MFMA column sub-tiles per wave)
-constexpr int BM_XB = 8;         // trial pairs per block (one per wave)
+// Block shapes (NW waves, one trial pair each; K-tile of 4 NW grid points):
+//   NW 8: 512 threads, 32-point K-tiles, one block per CU (118 KB LDS at TM 7)
+//   NW 4: 256 threads, 16-point K-tiles, two blocks per CU (59 KB each): the other
+//         block's MFMAs run through one block's barrier / staging phase
 
 // LDS images (doubles), one buffer:
 //   A  [g 32][i 16 TM]        swizzle i ^ 16 (g & 1) for even TM (odd TM: the row pitch
 //                             16 TM = 16 mod 32 doubles already separates the halves)
 //   W  [c 3][g 32][a 32]      swizzle a ^ 16 (g & 1)
 //   R  [g 32][xg 8][c 3]      (broadcast reads)
-template <int TM>
+template <int TM, int NW>
 struct BmLds {
-  static constexpr int A = BM_BK * 16 * TM;
-  static constexpr int W = 3 * BM_BK * BM_AB;
-  static constexpr int R = BM_BK * BM_XB * 3;
+  static constexpr int BK = 4 * NW, XB = NW;
+  static constexpr int A = BK * 16 * TM;
+  static constexpr int W = 3 * BK * BM_AB;
+  static constexpr int R = BK * XB * 3;
   static constexpr int BUF = A + W + R;
 };
 
@@ -68,17 +71,19 @@ __device__ __forceinline__ double rows4_m(double v) {
 // (TM - 1) + RV); those rows are accumulated on the VALU (RV x 2 FMAs per k-step
 // against the same B fragments, ~55 cycles at RV = 5) instead of a 16-row MFMA
 // sub-tile (2 MFMAs, ~145 cycles), and reduced over the four k-rows once per block.
-template <int TM, bool GEN_FIRST, int RV = 0>
-__global__ void __launch_bounds__(512, 1)
+template <int TM, bool GEN_FIRST, int RV = 0, int NW = 8>
+__global__ void __launch_bounds__(64 * NW, 1)
 k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
             const double* __restrict__ PO, long ldp,
             const double* __restrict__ Wg, long wc, long wg,
             const double* __restrict__ R, long rg,
             double* __restrict__ out, long ldo, long slab) {
-  using L = BmLds<TM>;
+  using L = BmLds<TM, NW>;
+  constexpr int BM_BK = L::BK, BM_XB = L::XB, NT = 64 * NW;
+  constexpr int R_LD = (L::R + NT - 1) / NT;
   constexpr int PA = 16 * TM;                  // A row length (i)
-  constexpr int A_LD = BM_BK * PA / 512;       // = TM doubles per thread
-  constexpr int W_LD = 3 * BM_BK * BM_AB / 512;  // = 6
+  constexpr int A_LD = BM_BK * PA / NT;        // = TM doubles per thread
+  constexpr int W_LD = 3 * BM_BK * BM_AB / NT;   // = 6
   constexpr int SWA = TM % 2 == 0 ? 16 : 0;    // A-image swizzle (see BmLds)
   __shared__ __attribute__((aligned(16))) double sm[2 * L::BUF];
 
@@ -113,25 +118,25 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
   //    consecutive i (one 128-B global segment, one conflict-free ds_write_b64 group)
   // W: element e -> (c, g, a) with a fastest over 32
   // R: element e -> (g, xg_l, c), 768 values, threads 0..255 load a second one
-  double ra[A_LD], rw[W_LD], rr[2];
+  double ra[A_LD], rw[W_LD], rr[R_LD];
   // per-thread byte offsets from the K-tile's (wave-uniform) row bases, columns
   // clamped once here.  Rows past n of the last K-tile are read unclamped: the
   // callers keep BM_BK rows of zeroed slack after the grid arrays (XC_GRID_SLACK),
   // and those rows' wv are stored as zero, so they add nothing.
-  unsigned oa[A_LD], ow[W_LD], orr[2];
+  unsigned oa[A_LD], ow[W_LD], orr[R_LD];
 #pragma unroll
   for (int e = 0; e < A_LD; ++e) {
-    const int p = tid + 512 * e, gl = p / PA, i = p % PA;
+    const int p = tid + NT * e, gl = p / PA, i = p % PA;
     oa[e] = (unsigned)(((long)gl * ldp + min(i, O - 1)) * 8);
   }
 #pragma unroll
   for (int e = 0; e < W_LD; ++e) {
-    const int p = tid + 512 * e, gl = (p / BM_AB) % BM_BK, al = p % BM_AB;
+    const int p = tid + NT * e, gl = (p / BM_AB) % BM_BK, al = p % BM_AB;
     ow[e] = (unsigned)(((long)gl * wg + min(a0 + al, V - 1)) * 8);
   }
 #pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int p = min(tid + 512 * e, L::R - 1), gl = p / (3 * BM_XB), xc = p % (3 * BM_XB);
+  for (int e = 0; e < R_LD; ++e) {
+    const int p = min(tid + NT * e, L::R - 1), gl = p / (3 * BM_XB), xc = p % (3 * BM_XB);
     orr[e] = (unsigned)(((long)gl * rg + 3 * min(x0 + xc / 3, nx - 1) + xc % 3) * 8);
   }
   auto ld8 = [](const double* base, unsigned off) XT_INLINE {
@@ -146,7 +151,7 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
 #pragma unroll
     for (int e = 0; e < W_LD; ++e) rw[e] = ld8(Wg + (e / 2) * wc + (long)g0 * wg, ow[e]);
 #pragma unroll
-    for (int e = 0; e < 2; ++e) rr[e] = ld8(pr, orr[e]);
+    for (int e = 0; e < R_LD; ++e) rr[e] = ld8(pr, orr[e]);
   };
   // zeros make the padding inert: grid points past n (R = 0 -> B = 0), virtuals
   // past V and pairs past nx (their columns are never stored; zero keeps them finite)
@@ -155,17 +160,17 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
     const int g0 = kt * BM_BK;
 #pragma unroll
     for (int e = 0; e < A_LD; ++e) {
-      const int p = tid + 512 * e, gl = p / PA, i = p % PA;
+      const int p = tid + NT * e, gl = p / PA, i = p % PA;
       s[gl * PA + (i ^ ((gl & 1) * SWA))] = ra[e];
     }
 #pragma unroll
     for (int e = 0; e < W_LD; ++e) {
-      const int p = tid + 512 * e, c = p / (BM_BK * BM_AB), gl = (p / BM_AB) % BM_BK, al = p % BM_AB;
+      const int p = tid + NT * e, c = p / (BM_BK * BM_AB), gl = (p / BM_AB) % BM_BK, al = p % BM_AB;
       s[L::A + (c * BM_BK + gl) * BM_AB + (al ^ ((gl & 1) << 4))] = a0 + al < V ? rw[e] : 0.0;
     }
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int p = tid + 512 * e;
+    for (int e = 0; e < R_LD; ++e) {
+      const int p = tid + NT * e;
       if (p < L::R) {
         const int gl = p / (3 * BM_XB), xc = p % (3 * BM_XB);
         s[L::A + L::W + p] = (g0 + gl < n && x0 + xc / 3 < nx) ? rr[e] : 0.0;
@@ -304,93 +309,114 @@ __global__ void k_xc_back_m_reduce(int O, long cols, int nsplit, const double* _
   }
 }
 
-// Split count: the fewest splits whose blocks fill the chip's 256 CUs in whole rounds
-// (within 3 %) while keeping >= 16 K-tiles per split.
-static int back_m_splits(int tiles, int nkt) {
+// Split count: the fewest splits whose blocks fill the chip's block slots (256 CUs x
+// blocks per CU) in whole rounds (within 3 %) while keeping >= 16 K-tiles per split.
+static int back_m_splits(int tiles, int nkt, int slots) {
   int best = 1;
   double best_eff = 0.0;
   for (int s = 1; s <= 64; ++s) {
     if (s > 1 && nkt / s < 16) break;
     const long blocks = (long)tiles * s;
-    const double rounds = (double)blocks / 256.0;
-    const double eff = rounds / ((blocks + 255) / 256);
+    const double rounds = (double)blocks / slots;
+    const double eff = rounds / ((blocks + slots - 1) / slots);
     if (eff > best_eff + 0.03 || (best_eff < 0.97 && eff > best_eff)) { best_eff = eff; best = s; }
-    if (eff >= 0.97 && blocks >= 512) break;
+    if (eff >= 0.97 && blocks >= 2 * slots) break;
   }
   return best;
 }
 
-size_t xc_back_m_workspace_bytes(int O, int nx, int V, int n) {
-  const int tiles = ((nx + BM_XB - 1) / BM_XB) * ((V + BM_AB - 1) / BM_AB);
-  const int s = back_m_splits(tiles, (n + BM_BK - 1) / BM_BK);
-  return sizeof(double) * (size_t)s * O * (size_t)nx * V;
+// block shape: XT_M_NW=4 selects the 4-wave, two-blocks-per-CU shape (measured
+// 167.7 vs 161.4 ms/step for the 8-wave shape on the same box: hiding one block's
+// barrier under the other's MFMAs does not pay for twice the barriers and A-tile loads)
+static int back_m_nw() {
+  const char* e = getenv("XT_M_NW");
+  return (e && atoi(e) == 4) ? 4 : 8;
 }
 
-template <int TM, int RV>
+struct BackMPlan { int nw, tiles, nkt, splits, kps, used, blocks; };
+static BackMPlan back_m_plan(int nx, int V, int n) {
+  BackMPlan p;
+  p.nw = back_m_nw();
+  const int bk = 4 * p.nw, xb = p.nw;
+  p.tiles = ((nx + xb - 1) / xb) * ((V + BM_AB - 1) / BM_AB);
+  p.nkt = (n + bk - 1) / bk;
+  p.splits = back_m_splits(p.tiles, p.nkt, p.nw == 4 ? 512 : 256);
+  p.kps = (p.nkt + p.splits - 1) / p.splits;
+  p.used = (p.nkt + p.kps - 1) / p.kps;
+  p.blocks = p.tiles * p.used;
+  return p;
+}
+
+size_t xc_back_m_workspace_bytes(int O, int nx, int V, int n) {
+  const BackMPlan p = back_m_plan(nx, V, n);
+  return sizeof(double) * (size_t)p.splits * O * (size_t)nx * V;
+}
+
+template <int TM, int RV, int NW>
 static void launch_back_m_rv(int O, int nx, int V, int n, int kps, int blocks, const double* PO, long ldp,
                              const double* W, long wc, long wg, const double* R, long rg, double* ws, long slab,
                              hipStream_t st) {
-  hipLaunchKernelGGL((k_xc_back_m<TM, false, RV>), dim3(blocks), dim3(512), 0, st, O, nx, V, n, kps, PO, ldp, W, wc,
-                     wg, R, rg, ws, (long)nx * V, slab);
+  hipLaunchKernelGGL((k_xc_back_m<TM, false, RV, NW>), dim3(blocks), dim3(64 * NW), 0, st, O, nx, V, n, kps, PO,
+                     ldp, W, wc, wg, R, rg, ws, (long)nx * V, slab);
 }
 
 // remainder rows on the VALU for the occupied counts of the BASELINE shapes
 // (O = 33..40: C2, C5; O = 97..104: the headline); XT_M_RV=0 keeps 16-row MFMA tiles
-template <int TM>
+template <int TM, int NW>
 static bool launch_back_m_valu(int O, int nx, int V, int n, int kps, int blocks, const double* PO, long ldp,
                                const double* W, long wc, long wg, const double* R, long rg, double* ws, long slab,
                                hipStream_t st) {
   const int rv = O - 16 * (TM - 1);
   if (TM == 7 && rv > 6) return false;                 // (spills at 256 VGPRs)
-#define XT_RV(N) case N: launch_back_m_rv<TM, N>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); return true;
+#define XT_RV(N) case N: launch_back_m_rv<TM, N, NW>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); return true;
   switch (rv) { XT_RV(1) XT_RV(2) XT_RV(3) XT_RV(4) XT_RV(5) XT_RV(6) XT_RV(7) XT_RV(8) default: return false; }
 #undef XT_RV
 }
 
-template <int TM>
+template <int TM, int NW>
 static void launch_back_m(int O, int nx, int V, int n, int kps, int blocks, const double* PO, long ldp,
                           const double* W, long wc, long wg, const double* R, long rg, double* ws, long slab,
                           hipStream_t st) {
-  static const int rv_on = [] { const char* e = getenv("XT_M_RV"); return e ? atoi(e) : 1; }();
+  const char* erv = getenv("XT_M_RV");
+  const int rv_on = erv ? atoi(erv) : 1;
   if constexpr (TM == 3 || TM == 7) {
-    if (rv_on && launch_back_m_valu<TM>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st)) return;
+    if (rv_on && launch_back_m_valu<TM, NW>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st))
+      return;
   }
-  static const int gen_first = [] { const char* e = getenv("XT_M_GEN"); return e ? atoi(e) : 0; }();
-  if (gen_first)
-    hipLaunchKernelGGL((k_xc_back_m<TM, true>), dim3(blocks), dim3(512), 0, st, O, nx, V, n, kps, PO, ldp, W, wc, wg,
-                       R, rg, ws, (long)nx * V, slab);
+  const char* eg = getenv("XT_M_GEN");
+  if (eg && atoi(eg) == 1)
+    hipLaunchKernelGGL((k_xc_back_m<TM, true, 0, NW>), dim3(blocks), dim3(64 * NW), 0, st, O, nx, V, n, kps, PO,
+                       ldp, W, wc, wg, R, rg, ws, (long)nx * V, slab);
   else
-    hipLaunchKernelGGL((k_xc_back_m<TM, false>), dim3(blocks), dim3(512), 0, st, O, nx, V, n, kps, PO, ldp, W, wc, wg,
-                     R, rg, ws, (long)nx * V, slab);
+    hipLaunchKernelGGL((k_xc_back_m<TM, false, 0, NW>), dim3(blocks), dim3(64 * NW), 0, st, O, nx, V, n, kps, PO,
+                       ldp, W, wc, wg, R, rg, ws, (long)nx * V, slab);
+}
+
+template <int NW>
+static void launch_back_m_tm(int TM, int O, int nx, int V, int n, int kps, int blocks, const double* PO, long ldp,
+                             const double* W, long wc, long wg, const double* R, long rg, double* ws, long slab,
+                             hipStream_t st) {
+#define XT_TM(N) case N: launch_back_m<N, NW>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+  switch (TM) { XT_TM(1) XT_TM(2) XT_TM(3) XT_TM(4) XT_TM(5) XT_TM(6) XT_TM(7) default: XT_TM(8) }
+#undef XT_TM
 }
 
 int xc_back_m(int O, int nx, int V, int n, const double* PO, long ldp, const double* W, long wc, long wg,
               const double* R, long rg, double* C, long ldc, double* ws, size_t ws_bytes, hipStream_t st) {
   if (O <= 0 || nx <= 0 || V <= 0 || n <= 0) return 0;
   if (O > 128) return XT_ERR_ARG;                      // one row tile (the engine's mode 2 covers more)
-  const int tiles = ((nx + BM_XB - 1) / BM_XB) * ((V + BM_AB - 1) / BM_AB);
-  const int nkt = (n + BM_BK - 1) / BM_BK;
-  const int s = back_m_splits(tiles, nkt);
+  const BackMPlan p = back_m_plan(nx, V, n);
   const long slab = (long)O * nx * V;
-  if (ws_bytes < sizeof(double) * (size_t)s * slab) return XT_ERR_ARG;
-  const int kps = (nkt + s - 1) / s;
-  const int used = (nkt + kps - 1) / kps;              // splits that own K-tiles
-  const int blocks = tiles * used;
+  if (ws_bytes < sizeof(double) * (size_t)p.splits * slab) return XT_ERR_ARG;
   const int TM = (O + 15) / 16;
-  switch (TM) {
-    case 1: launch_back_m<1>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
-    case 2: launch_back_m<2>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
-    case 3: launch_back_m<3>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
-    case 4: launch_back_m<4>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
-    case 5: launch_back_m<5>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
-    case 6: launch_back_m<6>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
-    case 7: launch_back_m<7>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
-    default: launch_back_m<8>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
-  }
+  if (p.nw == 4)
+    launch_back_m_tm<4>(TM, O, nx, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st);
+  else
+    launch_back_m_tm<8>(TM, O, nx, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st);
   const long total = slab;
   int rb = (int)((total + 255) / 256);
   if (rb > 8192) rb = 8192;
-  hipLaunchKernelGGL(k_xc_back_m_reduce, dim3(rb), dim3(256), 0, st, O, (long)nx * V, used, ws, slab, C, ldc);
+  hipLaunchKernelGGL(k_xc_back_m_reduce, dim3(rb), dim3(256), 0, st, O, (long)nx * V, p.used, ws, slab, C, ldc);
   return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
 }
 
