@@ -8,6 +8,7 @@
 //   U/S  (ncomp, G, nz*O)    per grid chunk: U_c = PhiV^c Ze^T, overwritten
 //                            in place by the back-projection factors S_c.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include "xt_internal.h"
 #include "xt_kernels.h"
 
@@ -555,6 +556,63 @@ k_xc_sf(int G, int g0, int nz, int O, int nmo, const double* __restrict__ phio,
   for (int i = lane; i < O; i += 64) u[i] = wv * ph[i];
 }
 
+// Same ALDA0 contraction, one wave per grid point for all nz trial vectors: the
+// point's occupied MO values stay in registers (IC chunks of 64 orbitals per lane),
+// 8 vectors' rows are loaded together and their 8 partial sums reduced by one
+// transposing butterfly (wave_sum_transpose<8>) instead of 8 x 6 shuffles; the
+// next group's rows are loaded before this group's reduction.  HBM-bound on U.
+template <int IC>
+__global__ void __launch_bounds__(256)
+k_xc_sf_pt(int G, int g0, int nz, int O, int nmo, const double* __restrict__ phio,
+           const double* __restrict__ fsf, double* __restrict__ U) {
+  constexpr int NV = 8;
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= G) return;   // whole waves only; no block-level synchronisation below
+  const long gg = g0 + g;
+  double ph[IC];
+#pragma unroll
+  for (int m = 0; m < IC; ++m) {
+    const int i = lane + 64 * m;
+    ph[m] = i < O ? phio[gg * nmo + i] : 0.0;
+  }
+  const double f = fsf[gg];
+  double* ub = U + (long)g * nz * O;
+  double un[NV][IC];
+  auto load = [&](int x0) {
+#pragma unroll
+    for (int xx = 0; xx < NV; ++xx)
+#pragma unroll
+      for (int m = 0; m < IC; ++m) {
+        const int i = lane + 64 * m, x = x0 + xx;
+        un[xx][m] = (x < nz && i < O) ? ub[(long)x * O + i] : 0.0;
+      }
+  };
+  load(0);
+  for (int x0 = 0; x0 < nz; x0 += NV) {
+    double v[NV];
+#pragma unroll
+    for (int xx = 0; xx < NV; ++xx) {
+      double a = 0.0;
+#pragma unroll
+      for (int m = 0; m < IC; ++m) a += un[xx][m] * ph[m];
+      v[xx] = a;
+    }
+    if (x0 + NV < nz) load(x0 + NV);
+    const double tot = wave_sum_transpose<NV>(v, lane);
+#pragma unroll
+    for (int xx = 0; xx < NV; ++xx) {
+      const int x = x0 + xx;
+      const double wv = readlane_d(tot, xx << 3) * f;
+#pragma unroll
+      for (int m = 0; m < IC; ++m) {
+        const int i = lane + 64 * m;
+        if (x < nz && i < O) ub[(long)x * O + i] = wv * ph[m];
+      }
+    }
+  }
+}
+
 // wfxc = fxc * w  (fxc layout (2,nc,2,nc,ngrid))
 __global__ void k_weight_fxc(long n4, int ngrid, const double* __restrict__ w, double* __restrict__ f) {
   GRID_STRIDE(t, n4 * ngrid) f[t] *= w[t % ngrid];
@@ -770,6 +828,14 @@ void xc_uks_w(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O
                        pO0, pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1);
 }
 void xc_sf(hipStream_t st, int G, int g0, int nz, int O, int nmo, const double* phio, const double* fsf, double* U) {
+  const char* e = getenv("XT_SF_POINT");
+  if (!(e && atoi(e) == 0) && O <= 256) {
+    const dim3 grid((G + 3) / 4), blk(256);
+    if (O <= 128)      hipLaunchKernelGGL((k_xc_sf_pt<2>), grid, blk, 0, st, G, g0, nz, O, nmo, phio, fsf, U);
+    else if (O <= 192) hipLaunchKernelGGL((k_xc_sf_pt<3>), grid, blk, 0, st, G, g0, nz, O, nmo, phio, fsf, U);
+    else               hipLaunchKernelGGL((k_xc_sf_pt<4>), grid, blk, 0, st, G, g0, nz, O, nmo, phio, fsf, U);
+    return;
+  }
   const long waves = (long)G * nz;
   const int blocks = (int)((waves * 64 + 255) / 256);
   hipLaunchKernelGGL(k_xc_sf, dim3(blocks), dim3(256), 0, st, G, g0, nz, O, nmo, phio, fsf, U);
