@@ -8,6 +8,8 @@ the row counts that take its 160-row streaming tile and its batching.
   (default: the dedicated kernel, xt_xcw.hip)
 * XT_XSF_FUSED=0 -> XSF Delta-A exchange as direct DF sandwiches
   (default with the stored exchange: one Kx stream for main + Delta-A exchange)
+* XT_SKINNY_RV=0 -> 33..40-row stored exchange through the 48-row MFMA tile
+  (default: 32 MFMA rows + up to 8 VALU remainder rows)
 Tolerance: 1e-12 relative max-norm on sigma (FP64 round-off of a different
 summation order), as in test_gpu_parity.py.
 """
@@ -74,4 +76,18 @@ def test_xsf_stored_exchange_blocks(hiplib, env, nz, sa, fused):
     z = make_trial_vectors(nz, hdiag.size)
     op = DeviceOperator(mf, "XSF", sa=sa, fglobal=fg, foo=0.7, remove=o.re, k_mode="stored")
     op.set_oo_basis(o.vects)
+    assert rel(op.apply(z), vind(z)) < RTOL
+
+
+@pytest.mark.parametrize("nz", [17, 20])
+@pytest.mark.parametrize("rv", [1, 0])
+def test_stored_exchange_row_shapes(hiplib, env, nz, rv):
+    """2 nz = 34 / 40 rows: the 32 MFMA rows + VALU remainder shape of the streaming
+    exchange kernel (XT_SKINNY_RV=1, default) and the 48-row MFMA shape."""
+    from xtddft_amd.operator import DeviceOperator
+    env(XT_SKINNY_RV=rv)
+    mf = make_mf(nao=40, nc=8, no=2, ngrid=2000, xctype="GGA", hyb=0.25)
+    vind, hdiag = oxtda.gen_tda_operation(mf)
+    z = make_trial_vectors(nz, hdiag.size)
+    op = DeviceOperator(mf, "XTDA", k_mode="stored")
     assert rel(op.apply(z), vind(z)) < RTOL

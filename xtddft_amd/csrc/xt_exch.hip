@@ -24,6 +24,7 @@
 // K splits write partial sums to a workspace; skinny_reduce adds them in a
 // fixed order (deterministic) and applies alpha / beta.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include "xt_internal.h"
 
 namespace xt {
@@ -40,11 +41,15 @@ constexpr int SK_MAXM = 160;
 
 // SK_D: B prefetch ring depth in k-steps (Kx streams from HBM: the ring has to
 // cover an HBM miss under full load, ~2-4 us, with 8 waves per CU)
-template <int SK_TM, int SK_TN, int SK_BK, int SK_D>
+// SK_RV > 0: rows 16 SK_TM .. 16 SK_TM + SK_RV - 1 (the A image keeps a third 16-row
+// block) are accumulated on the VALU against the same B values (SK_RV x SK_TN FMAs
+// per k-step instead of SK_TN MFMAs on a mostly empty 16-row sub-tile) and reduced
+// over the four k-rows at the end: M = 40 (the headline's 2 nz) as 32 + 8.
+template <int SK_TM, int SK_TN, int SK_BK, int SK_D, int SK_RV = 0>
 __global__ void __launch_bounds__(512, SK_TM <= 3 ? 2 : 1)
 k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
          const double* __restrict__ B, long ldb, double* __restrict__ out, long ldo) {
-  constexpr int SK_MP = 16 * SK_TM;                // padded rows
+  constexpr int SK_MP = 16 * SK_TM + (SK_RV ? 16 : 0);   // rows of the A image
   constexpr int SK_BN = 16 * SK_TN * SK_WAVES;     // columns per block
   constexpr int A_PIECES = SK_BK * SK_MP / 2;      // 16-B pieces per chunk
   static_assert(A_PIECES % 512 == 0, "A staging map");
@@ -70,6 +75,12 @@ k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
   for (int i = 0; i < SK_TM; ++i)
 #pragma unroll
     for (int j = 0; j < SK_TN; ++j) acc[i][j] = (d4x){0.0, 0.0, 0.0, 0.0};
+  constexpr int RVA = SK_RV ? SK_RV : 1;
+  double part[RVA][SK_TN];
+#pragma unroll
+  for (int i = 0; i < RVA; ++i)
+#pragma unroll
+    for (int j = 0; j < SK_TN; ++j) part[i][j] = 0.0;
 
   // A chunk staging: SK_BK k x SK_MP m doubles in 16-B pieces, A_E per thread; rows
   // past this split's k1 are zero, which makes whole chunks safe at the end
@@ -131,6 +142,15 @@ k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
         for (int i = 0; i < SK_TM; ++i) af[i] = As[buf][kk * SK_MP + 16 * i + r];
         const bvec bv = bq[u];
         load_b(s + SK_D, bq[u]);                     // refill this ring slot
+        if constexpr (SK_RV > 0) {
+          const double* ar = &As[buf][kk * SK_MP + 16 * SK_TM];   // broadcast over the 16 lanes of a k-row
+#pragma unroll
+          for (int i = 0; i < SK_RV; ++i) {
+            const double av = ar[i];
+#pragma unroll
+            for (int j = 0; j < SK_TN; ++j) part[i][j] += av * bv[j];
+          }
+        }
 #pragma unroll
         for (int i = 0; i < SK_TM; ++i)
 #pragma unroll
@@ -144,9 +164,43 @@ k_skinny(int N, int K, int kchunk, const double* __restrict__ AT,
     store_a(buf ^ 1);
     __syncthreads();
   }
+  // the VALU rows: sum the four k-rows (lanes r, r+16, r+32, r+48), every lane
+  if constexpr (SK_RV > 0) {
+#pragma unroll
+    for (int i = 0; i < SK_RV; ++i)
+#pragma unroll
+      for (int j = 0; j < SK_TN; ++j) {
+        double v = part[i][j];
+        auto pair = [](double x, bool p32) XT_INLINE {
+          const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+          const auto a = p32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                             : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+          const auto b = p32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                             : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+          return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+        };
+        part[i][j] = pair(pair(v, false), true);
+      }
+  }
   // C/D layout: col = lane & 15 (= r), row = 4 reg + q; sub-tile j col r -> TN r + j
   if (c0 >= N) return;
   double* o = out + (long)split * SK_MP * ldo;
+  if constexpr (SK_RV > 0) {
+    if (q == 0) {
+#pragma unroll
+      for (int i = 0; i < SK_RV; ++i) {
+        const int m = 16 * SK_TM + i;
+        if (c0 + SK_TN - 1 < N) {
+#pragma unroll
+          for (int j = 0; j < SK_TN; j += 2)
+            *(d2x*)(o + (long)m * ldo + c0 + j) = (d2x){part[i][j], part[i][j + 1]};
+        } else {
+#pragma unroll
+          for (int j = 0; j < SK_TN; ++j) if (c0 + j < N) o[(long)m * ldo + c0 + j] = part[i][j];
+        }
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < SK_TM; ++i)
 #pragma unroll
@@ -234,7 +288,12 @@ int skinny_gemm(int M, int N, int K, double alpha, const double* A, long lda, co
                      dim3(256), 0, st, M, K, sh.bk, sh.mp, A, lda, AT);
   const int strips = (N + sh.bn - 1) / sh.bn;
   const int used = (K + kchunk - 1) / kchunk;
-  if (sh.mp == 48)
+  const char* erv = getenv("XT_SKINNY_RV");
+  const bool rv = !(erv && atoi(erv) == 0) && M > 32 && M <= 40;
+  if (sh.mp == 48 && rv)
+    hipLaunchKernelGGL((k_skinny<2, 4, 64, 4, 8>), dim3(strips, used), dim3(512), 0, st, N, K, kchunk, AT, B, ldb,
+                       part, (long)N);
+  else if (sh.mp == 48)
     hipLaunchKernelGGL((k_skinny<3, 4, 64, 4>), dim3(strips, used), dim3(512), 0, st, N, K, kchunk, AT, B, ldb, part,
                        (long)N);
   else
