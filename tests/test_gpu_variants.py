@@ -6,6 +6,9 @@ the row counts that take its 160-row streaming tile and its batching.
   (default: the dedicated kernel, xt_xcm.hip)
 * XT_W_KERNEL=0  -> XC rho-forward through the generic engine's mode 1
   (default: the dedicated kernel, xt_xcw.hip)
+* XT_W_RING=0    -> the dedicated rho-forward kernel's select-based ring advance
+* XT_M_WAB=0     -> dedicated M-backward with the next K-tile's LDS writes before the
+  closing barrier (default: after the opening one)
 * XT_XSF_FUSED=0 -> XSF Delta-A exchange as direct DF sandwiches
   (default with the stored exchange: one Kx stream for main + Delta-A exchange)
 * XT_SKINNY_RV=0 -> 33..40-row stored exchange through the 48-row MFMA tile
@@ -47,7 +50,8 @@ def env():
 
 
 @pytest.mark.parametrize("knobs", [dict(XT_M_KERNEL=0), dict(XT_W_KERNEL=0), dict(XT_M_KERNEL=0, XT_W_KERNEL=0),
-                                   dict(XT_M_KERNEL=1, XT_W_KERNEL=1), dict(XT_W_RING=0)])
+                                   dict(XT_M_KERNEL=1, XT_W_KERNEL=1), dict(XT_W_RING=0),
+                                   dict(XT_M_WAB=0)])
 @pytest.mark.parametrize("nc,no,nao", [(5, 2, 26), (33, 1, 60), (35, 2, 70), (95, 2, 130), (99, 2, 140),
                                       (120, 3, 150)])
 def test_xc_kernel_variants(hiplib, env, knobs, nc, no, nao):

@@ -71,7 +71,7 @@ __device__ __forceinline__ double rows4_m(double v) {
 // (TM - 1) + RV); those rows are accumulated on the VALU (RV x 2 FMAs per k-step
 // against the same B fragments, ~55 cycles at RV = 5) instead of a 16-row MFMA
 // sub-tile (2 MFMAs, ~145 cycles), and reduced over the four k-rows once per block.
-template <int TM, bool GEN_FIRST, int RV = 0, int NW = 8>
+template <int TM, bool GEN_FIRST, int RV = 0, int NW = 8, bool WAB = false>
 __global__ void __launch_bounds__(64 * NW, 1)
 k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
             const double* __restrict__ PO, long ldp,
@@ -254,7 +254,23 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
   };
   (void)a_lane;
 
-  if (kt0 < kt1) {
+  if (WAB && kt0 < kt1) {
+    // K-tile kt + 1 is written to LDS right after the barrier that opens K-tile kt (its
+    // buffer was last read by K-tile kt - 1) and kt + 2 is loaded right after: the
+    // stores overlap the other waves' MFMAs instead of delaying the barrier
+    load(kt0);
+    store(0, kt0);
+    if (kt0 + 1 < kt1) load(kt0 + 1);
+    __syncthreads();
+    int buf = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      if (kt + 1 < kt1) store(buf ^ 1, kt + 1);
+      if (kt + 2 < kt1) load(kt + 2);
+      if (wave_on) compute(buf);
+      __syncthreads();
+      buf ^= 1;
+    }
+  } else if (kt0 < kt1) {
     load(kt0);
     store(0, kt0);
     __syncthreads();
@@ -356,8 +372,16 @@ template <int TM, int RV, int NW>
 static void launch_back_m_rv(int O, int nx, int V, int n, int kps, int blocks, const double* PO, long ldp,
                              const double* W, long wc, long wg, const double* R, long rg, double* ws, long slab,
                              hipStream_t st) {
-  hipLaunchKernelGGL((k_xc_back_m<TM, false, RV, NW>), dim3(blocks), dim3(64 * NW), 0, st, O, nx, V, n, kps, PO,
-                     ldp, W, wc, wg, R, rg, ws, (long)nx * V, slab);
+  // XT_M_WAB=0: LDS writes of the next K-tile before the barrier that closes this one
+  // (measured 1 % slower at the headline: 161.9-163.2 vs 159.8-160.9 ms/step)
+  const char* ewab = getenv("XT_M_WAB");      // read per call: tests switch it in-process
+  const int wab = ewab ? atoi(ewab) : 1;
+  if (wab)
+    hipLaunchKernelGGL((k_xc_back_m<TM, false, RV, NW, true>), dim3(blocks), dim3(64 * NW), 0, st, O, nx, V, n, kps,
+                       PO, ldp, W, wc, wg, R, rg, ws, (long)nx * V, slab);
+  else
+    hipLaunchKernelGGL((k_xc_back_m<TM, false, RV, NW>), dim3(blocks), dim3(64 * NW), 0, st, O, nx, V, n, kps, PO,
+                       ldp, W, wc, wg, R, rg, ws, (long)nx * V, slab);
 }
 
 // remainder rows on the VALU for the occupied counts of the BASELINE shapes
