@@ -55,7 +55,7 @@ __device__ __forceinline__ double rows4(double v) {
 }
 
 template <int TNG, bool BRANCHY>
-__global__ void __launch_bounds__(512, 1)
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TNG <= 2 ? 4 : 2, TNG <= 2 ? 4 : 2)))
 k_xc_rho_w(int O, int nx, int V, int n,
            const double* __restrict__ PO, long ldp,
            const double* __restrict__ Z, long zi, long zx,
@@ -254,38 +254,54 @@ k_xc_rho_w(int O, int nx, int V, int n,
   }
 }
 
-static constexpr int kWTng = 4;
+static int w_tng() {                           // XT_W_TNG=2: 32-point blocks, two per CU
+  const char* e = getenv("XT_W_TNG");          // read per call: tests switch it in-process
+  return e && atoi(e) == 2 ? 2 : 4;
+}
 
-size_t xc_rho_w_lds_bytes(int O) {
-  const int GB = 16 * kWTng;
+static size_t rho_w_lds(int O, int tng) {
+  const int GB = 16 * tng;
   return sizeof(double) * ((size_t)((O + 7) & ~7) * GB + 2 * 3 * WA * GB);
+}
+
+size_t xc_rho_w_lds_bytes(int O) { return rho_w_lds(O, w_tng()); }
+
+template <int TNG>
+static void launch_rho_w(int branchy, int blocks, size_t lds, hipStream_t st, int O, int nx, int V, int n,
+                         const double* PO, long ldp, const double* Z, long zi, long zx, const double* W, long wc,
+                         long wg, double* R, long rg) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_xc_rho_w<TNG, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_xc_rho_w<TNG, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
+  if (branchy)
+    hipLaunchKernelGGL((k_xc_rho_w<TNG, true>), dim3(blocks), dim3(512), lds, st, O, nx, V, n, PO, ldp, Z, zi, zx,
+                       W, wc, wg, R, rg);
+  else
+    hipLaunchKernelGGL((k_xc_rho_w<TNG, false>), dim3(blocks), dim3(512), lds, st, O, nx, V, n, PO, ldp, Z, zi,
+                       zx, W, wc, wg, R, rg);
 }
 
 int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const double* Z, long zi, long zx,
              const double* W, long wc, long wg, double* R, long rg, hipStream_t st) {
   if (O <= 0 || nx <= 0 || V <= 0 || n <= 0) return 0;
-  const size_t lds = xc_rho_w_lds_bytes(O);
+  const int tng = w_tng();
+  const size_t lds = rho_w_lds(O, tng);
   if (lds > 160 * 1024) return XT_ERR_ARG;
   // XT_W_RING=0: the select-based (branch-free) ring advance; measured slower on the
   // same box (178.2 vs 170.6 ms/step; engine mode 1: 173.4)
   const char* ering = getenv("XT_W_RING");    // read per call: tests switch it in-process
   const int branchy = ering ? atoi(ering) : 1;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_xc_rho_w<kWTng, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_xc_rho_w<kWTng, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr = true;
-  }
-  const int GB = 16 * kWTng;
+  const int GB = 16 * tng;
   const int blocks = ((n + GB - 1) / GB) * ((nx + WXB - 1) / WXB);
-  if (branchy)
-    hipLaunchKernelGGL((k_xc_rho_w<kWTng, true>), dim3(blocks), dim3(512), lds, st, O, nx, V, n, PO, ldp, Z, zi, zx,
-                       W, wc, wg, R, rg);
+  if (tng == 2)
+    launch_rho_w<2>(branchy, blocks, lds, st, O, nx, V, n, PO, ldp, Z, zi, zx, W, wc, wg, R, rg);
   else
-    hipLaunchKernelGGL((k_xc_rho_w<kWTng, false>), dim3(blocks), dim3(512), lds, st, O, nx, V, n, PO, ldp, Z, zi,
-                       zx, W, wc, wg, R, rg);
+    launch_rho_w<4>(branchy, blocks, lds, st, O, nx, V, n, PO, ldp, Z, zi, zx, W, wc, wg, R, rg);
   return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
 }
 
