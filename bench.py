@@ -517,7 +517,9 @@ def rank_main(args):
         dist.barrier()
     dt = time.perf_counter() - t0
     op.set_profile(0)
-    tt = torch.tensor([dt], dtype=torch.float64)
+    # RCCL reduces device tensors only (a host tensor raises under the nccl backend)
+    tt = torch.tensor([dt], dtype=torch.float64,
+                      device=w.device if (use_gpu and backend == "nccl") else "cpu")
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     T = float(tt.item())

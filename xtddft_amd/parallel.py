@@ -32,17 +32,28 @@ def allreduce_sigma(sigma, group=None):
     """Sum of the per-rank partial sigma over the process group.
 
     A torch tensor is reduced in place (through a host copy when the backend
-    is gloo and the tensor lives on the GPU); a NumPy array is reduced through
-    a CPU tensor and returned as a new array."""
+    is gloo and the tensor lives on the GPU, through a device copy when the
+    backend is RCCL and it lives on the host); a NumPy array is reduced the
+    same way and returned as a new array."""
     import numpy as np
     import torch
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1):
         return sigma
+    nccl = dist.get_backend(group) == "nccl"
     if isinstance(sigma, np.ndarray):
         t = torch.from_numpy(np.ascontiguousarray(sigma, dtype=np.float64))
+        if nccl:     # RCCL reduces device tensors only
+            d = t.to(f"cuda:{torch.cuda.current_device()}")
+            dist.all_reduce(d, group=group)
+            return d.cpu().numpy()
         dist.all_reduce(t, group=group)
         return t.numpy()
+    if not sigma.is_cuda and nccl:
+        d = sigma.to(f"cuda:{torch.cuda.current_device()}")
+        dist.all_reduce(d, group=group)
+        sigma.copy_(d)
+        return sigma
     if sigma.is_cuda and dist.get_backend(group) == "gloo":
         h = sigma.cpu()
         dist.all_reduce(h, group=group)
