@@ -174,6 +174,24 @@ int xt_row_norms2(int nrow, int dim, const double* x, double* out, void* hip_str
 /* x[i,:] *= s[i] */
 int xt_row_scale(int nrow, int dim, double* x, const double* s, void* hip_stream);
 
+/* mean-field front end ------------------------------ */
+/* 3-index Coulomb integrals (ab|c) over contracted Cartesian Gaussians by
+   McMurchie-Davidson (replaces libcint int3c2e behind PySCF df.incore.aux_e2,
+   the DF factor whose get_jk XTDA.py:518-543 calls and whose MO transform
+   stands in for ao2mo.general, XTDA.py:120).  Device pointers, launched on
+   `hip_stream`; `out` is accumulated into (zero it first).
+     pair_info[8k+0..5]  la, lb, npp, first row of pair_prim, offset in eab, first output row
+     pair_prim[4q+0..3]  p, Px, Py, Pz of primitive pair q
+     eab                 per pair [a][b][t][q]: Hermite coefficients x contraction coefficients
+     aux_info[8j+0..4]   lc, nprim, first row of aux_prim, offset in ek, first output column
+     aux_prim[4r+0..3]   exponent, Cx, Cy, Cz
+     ek                  per aux shell [c][u][r]: one-centre Hermite coefficients x coefficients
+     out[(row0 + a*ncart(lb) + b) * ldo + col0 + c] += (ab|c)
+   lmax_orb <= 2, lmax_aux <= 6. */
+int xt_int3c2e_cart(int npair, const int* pair_info, const double* pair_prim, const double* eab,
+                    int naux_shells, const int* aux_info, const double* aux_prim, const double* ek,
+                    int lmax_orb, int lmax_aux, double* out, long ldo, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

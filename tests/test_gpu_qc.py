@@ -58,3 +58,38 @@ def test_density_fitted_device_scf_and_xsf(torch):
     ref = reference_outputs()
     e, _ = XSF_TDA(mf).kernel(nstates=10, fglobal=ref["xsf_roks_alda0_fglobal"])
     assert np.abs(np.asarray(e) / HA2EV_XSF - np.asarray(ref["xsf_roks_alda0_ev"]) / HA2EV_XSF).max() < 5e-4
+
+
+def _spd_mol():
+    from xtddft_amd.qc import M
+    basis = {"O": [[0, [30.0, 0.3], [6.0, 0.7]], [0, [0.9, 1.0]], [1, [5.0, 0.4], [1.1, 0.7]],
+                   [2, [1.2, 1.0]]],
+             "H": [[0, [3.0, 0.4], [0.5, 0.7]], [1, [0.8, 1.0]]]}
+    atoms = [("O", (0.0, 0.0, 0.1)), ("H", (1.4, 1.0, 0.2)), ("H", (-1.3, 1.1, -0.4))]
+    return M(atoms, basis=basis, unit="Bohr")
+
+
+@pytest.mark.parametrize("which", ["hf_631g", "spd"])
+def test_device_int3c2e_equals_host(torch, which):
+    """The HIP 3-index integrals (csrc/xt_int.hip) against the host McMurchie-Davidson
+    routine (qc/ints.py eri3c, itself checked against the 4-index routine):
+    HF / 6-31G with its even-tempered auxiliary basis (aux l <= 3) and an s/p/d
+    molecule (aux l <= 5; exponents up to 30 put the Boys argument on both sides of
+    the series / asymptotic switch at T = 30).  Tolerance 1e-12 of the largest
+    integral (FP64 round-off of a different summation order)."""
+    from xtddft_amd.qc.df import aux_mole
+    mol = hf_mol() if which == "hf_631g" else _spd_mol()
+    aux = aux_mole(mol)
+    host = mol.int3c2e(aux)
+    dev = mol.int3c2e(aux, device=0)
+    assert dev.shape == host.shape
+    assert np.abs(dev - host).max() < 1e-12 * np.abs(host).max()
+
+
+def test_density_fitted_scf_with_device_integrals(torch):
+    """mf.density_fit() + mf.to_device(0): the DF factor's 3-index integrals come from
+    the GPU; the SCF energy equals the host DF SCF to 1e-10 Ha."""
+    host = _scf("ROKS", False, df=True)
+    dev = _scf("ROKS", True, df=True)
+    assert dev.with_df.device == 0
+    assert abs(dev.e_tot - host.e_tot) < 1e-10

@@ -9,6 +9,7 @@ the row counts that take its 160-row streaming tile and its batching.
 * XT_W_RING=0    -> the dedicated rho-forward kernel's select-based ring advance
 * XT_M_WAB=0     -> dedicated M-backward with the next K-tile's LDS writes before the
   closing barrier (default: after the opening one)
+* XT_W_TNG=2     -> dedicated rho-forward on 32-point blocks, two per CU
 * XT_XSF_FUSED=0 -> XSF Delta-A exchange as direct DF sandwiches
   (default with the stored exchange: one Kx stream for main + Delta-A exchange)
 * XT_SKINNY_RV=0 -> 33..40-row stored exchange through the 48-row MFMA tile

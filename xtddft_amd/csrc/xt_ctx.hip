@@ -1384,3 +1384,14 @@ extern "C" int xt_row_scale(int nrow, int dim, double* x, const double* s, void*
   row_scale((hipStream_t)stream, nrow, dim, x, s);
   return hipGetLastError() == hipSuccess ? 0 : fail(XT_ERR_HIP, "row_scale launch failed");
 }
+
+extern "C" int xt_int3c2e_cart(int npair, const int* pair_info, const double* pair_prim, const double* eab,
+                               int naux_shells, const int* aux_info, const double* aux_prim, const double* ek,
+                               int lmax_orb, int lmax_aux, double* out, long ldo, void* stream) {
+  if (npair < 0 || naux_shells < 0 || ldo < 0) return fail(XT_ERR_ARG, "xt_int3c2e_cart: negative size");
+  if (lmax_orb > kInt3cMaxLab || lmax_aux > kInt3cMaxLc)
+    return fail(XT_ERR_ARG, "xt_int3c2e_cart: orbital shells up to d and auxiliary shells up to l = 6");
+  const int r = int3c2e_cart(npair, pair_info, pair_prim, eab, naux_shells, aux_info, aux_prim, ek, out, ldo,
+                             (hipStream_t)stream);
+  return r ? fail(r, "int3c2e launch failed") : 0;
+}

@@ -88,6 +88,11 @@ int xc_back_m(int O, int nx, int V, int n, const double* PO, long ldp, const dou
 // PhiO[g][i] Zp[i zi + xg zx + a]; reads Zp up to 7 rows past O and WA - 1 columns past
 // V (zeroed slack), grid arrays XC_GRID_SLACK rows past n
 size_t xc_rho_w_lds_bytes(int O);
+// 3-index Coulomb integrals over Cartesian Gaussians (xt_int.hip); orbital l <= 2, aux l <= 6
+constexpr int kInt3cMaxLab = 2, kInt3cMaxLc = 6;
+int int3c2e_cart(int npair, const int* pair_info, const double* pair_prim, const double* eab, int naux_shells,
+                 const int* aux_info, const double* aux_prim, const double* ek, double* out, long ldo,
+                 hipStream_t st);
 int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const double* Z, long zi, long zx,
              const double* W, long wc, long wg, double* R, long rg, hipStream_t st);
 size_t dgemm_workspace_bytes(const GemmDesc& d);

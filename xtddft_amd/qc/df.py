@@ -92,16 +92,17 @@ def cholesky_cderi(j3: np.ndarray, j2: np.ndarray, lindep: float = 1e-12) -> np.
 class DF:
     """``mf.with_df``: auxiliary Mole and the 3-index factor."""
 
-    def __init__(self, mol, auxbasis=None):
+    def __init__(self, mol, auxbasis=None, device=None):
         self.mol = mol
         self.auxbasis = auxbasis
+        self.device = device            # GPU for the 3-index integrals (None: host)
         self.auxmol = None
         self._cderi = None
 
     def build(self):
         if self._cderi is None:
             self.auxmol = aux_mole(self.mol, self.auxbasis)
-            j3 = self.mol.int3c2e(self.auxmol)
+            j3 = self.mol.int3c2e(self.auxmol, device=self.device)
             j2 = self.auxmol.int2c2e()
             self._cderi = cholesky_cderi(j3, j2)
         return self

@@ -282,9 +282,13 @@ class Mole:
         return {l: (AuxShellSet([self.shells[k] for k in ks]), [int(self.ao_loc[k]) for k in ks])
                 for l, ks in groups.items()}
 
-    def int3c2e(self, auxmol) -> np.ndarray:
+    def int3c2e(self, auxmol, device=None) -> np.ndarray:
         """(P|mu nu) over normalised spherical functions: (naux, nao, nao) -- PySCF
-        ``df.incore.aux_e2(mol, auxmol, 'int3c2e')`` transposed to aux-major."""
+        ``df.incore.aux_e2(mol, auxmol, 'int3c2e')`` transposed to aux-major.
+        ``device=k``: evaluated on GPU k (``qc.dints``, the HIP integral kernel)."""
+        if device is not None:
+            from .dints import int3c2e_device
+            return int3c2e_device(self, auxmol, device)
         n, naux = self._nao, auxmol.nao
         out = np.zeros((naux, n, n))
         aux = auxmol._aux_groups()

@@ -60,6 +60,9 @@ class _SCFBase:
         self._device = device
         self.device_engine = None
         self._built = False
+        df = getattr(self, "with_df", None)
+        if df is not None and df._cderi is None:
+            df.device = device          # the 3-index integrals on the same GPU
         return self
 
     def density_fit(self, auxbasis=None):
@@ -67,7 +70,7 @@ class _SCFBase:
         ``mf.density_fit()``; the reference's DF mean fields, XTDA.py:518-543).
         ``auxbasis``: {element: shells} or None for the even-tempered default."""
         from .df import DF
-        self.with_df = DF(self.mol, auxbasis)
+        self.with_df = DF(self.mol, auxbasis, device=getattr(self, "_device", None))
         self._built = False
         return self
 
