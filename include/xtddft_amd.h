@@ -183,11 +183,14 @@ int xt_row_scale(int nrow, int dim, double* x, const double* s, void* hip_stream
      pair_info[8k+0..5]  la, lb, npp, first row of pair_prim, offset in eab, first output row
      pair_prim[4q+0..3]  p, Px, Py, Pz of primitive pair q
      eab                 per pair [a][b][t][q]: Hermite coefficients x contraction coefficients
-     aux_info[8j+0..4]   lc, nprim, first row of aux_prim, offset in ek, first output column
+     aux_info[8j+0..5]   lc, nprim, first row of aux_prim, offset in ek, first output column, nc
      aux_prim[4r+0..3]   exponent, Cx, Cy, Cz
      ek                  per aux shell [c][u][r]: one-centre Hermite coefficients x coefficients
      out[(row0 + a*ncart(lb) + b) * ldo + col0 + c] += (ab|c)
-   lmax_orb <= 2, lmax_aux <= 6. */
+   The ket may be a shell pair (4-index (ab|cd), the stored-ERI path of `jk_mode`
+   ERI8 / PySCF mol.intor('int2e')): lc = l_c + l_d, nc = ncart(l_c) ncart(l_d),
+   its primitive pairs in aux_prim and its pair Hermite coefficients in ek.
+   lmax_orb <= 2, lmax_aux <= 6 (the ket's Hermite order). */
 int xt_int3c2e_cart(int npair, const int* pair_info, const double* pair_prim, const double* eab,
                     int naux_shells, const int* aux_info, const double* aux_prim, const double* ek,
                     int lmax_orb, int lmax_aux, double* out, long ldo, void* hip_stream);

@@ -19,7 +19,7 @@
 namespace xt {
 
 constexpr int I3_MAXLAB = 4;                   // d shells on the orbital side
-constexpr int I3_MAXLC = 6;                    // auxiliary shells up to i
+constexpr int I3_MAXLC = 6;                    // auxiliary shells up to i (ket pairs up to d d)
 constexpr int I3_MAXL = I3_MAXLAB + I3_MAXLC;
 constexpr int I3_NTUV = (I3_MAXL + 1) * (I3_MAXL + 2) * (I3_MAXL + 3) / 6;
 constexpr int I3_NTAB = (I3_MAXLAB + 1) * (I3_MAXLAB + 2) * (I3_MAXLAB + 3) / 6;
@@ -90,9 +90,11 @@ __device__ void hermite_r(int L, double alpha, double X, double Y, double Z, dou
 }
 
 // pair_info[8 k + .]: la, lb, npp, prim0, e0, row0;  pair_prim[4 q + .]: p, Px, Py, Pz
-// aux_info[8 j + .]:  lc, nprim, prim0, e0, col0;    aux_prim[4 r + .]:  s, Cx, Cy, Cz
+// aux_info[8 j + .]:  lc, nprim, prim0, e0, col0, nc; aux_prim[4 r + .]:  s, Cx, Cy, Cz
 // eab (pair k): [a][b][t][q] over ncart(la) x ncart(lb) x ntuv(la+lb) x npp
-// ek (aux j):   [c][u][r]    over ncart(lc) x ntuv(lc) x nprim
+// ek (aux j):   [c][u][r]    over nc x ntuv(lc) x nprim
+// The ket may be a shell pair too (4-index (ab|cd)): lc = l_c + l_d, nc = ncart(l_c)
+// ncart(l_d) components, its primitive pairs and Hermite coefficients as the bra's.
 __global__ void __launch_bounds__(64)
 k_int3c2e_cart(int npair, const int* __restrict__ pair_info, const double* __restrict__ pair_prim,
                const double* __restrict__ eab, int naux, const int* __restrict__ aux_info,
@@ -106,7 +108,7 @@ k_int3c2e_cart(int npair, const int* __restrict__ pair_info, const double* __res
   const int la = pi[0], lb = pi[1], npp = pi[2], pq0 = pi[3], pe0 = pi[4], row0 = pi[5];
   const int lc = ai[0], nr = ai[1], ar0 = ai[2], ae0 = ai[3], col0 = ai[4];
   const int lab = la + lb, L = lab + lc;
-  const int nab = ncart(la) * ncart(lb), ntab = ntuv(lab), nc = ncart(lc), ntc = ntuv(lc);
+  const int nab = ncart(la) * ncart(lb), ntab = ntuv(lab), nc = ai[5], ntc = ntuv(lc);
   double R[I3_NTUV], S[I3_NTUV], M[I3_NTAB];
   for (int q = 0; q < npp; ++q) {
     const double* pp = pair_prim + 4 * (long)(pq0 + q);

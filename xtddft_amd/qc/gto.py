@@ -327,8 +327,12 @@ class Mole:
         nrm = self._norm
         return out * (nrm[:, None] * nrm[None, :])
 
-    def eri_full(self) -> np.ndarray:
-        """(mu nu|la si) over normalised spherical AOs, all 8 symmetry copies filled."""
+    def eri_full(self, device=None) -> np.ndarray:
+        """(mu nu|la si) over normalised spherical AOs, all 8 symmetry copies filled.
+        ``device=k``: evaluated on GPU k (``qc.dints``, the HIP integral kernel)."""
+        if device is not None:
+            from .dints import eri_full_device
+            return eri_full_device(self, device)
         n = self._nao
         sh = self.shells
         nsh = len(sh)

@@ -82,7 +82,7 @@ class _SCFBase:
         self.comps, self.hyb, self.xctype = _xc.parse_xc(self.xc)
         self.s1e = mol.intor("int1e_ovlp")
         self.h1e = mol.intor("int1e_kin") + mol.intor("int1e_nuc")
-        self.eri = mol.eri_full() if self.with_df is None else None
+        self.eri = mol.eri_full(device=getattr(self, "_device", None)) if self.with_df is None else None
         if self.with_df is not None:
             self.with_df.build()
         if self.xctype != "HF":
