@@ -9,7 +9,8 @@ the row counts that take its 160-row streaming tile and its batching.
 * XT_W_RING=0    -> the dedicated rho-forward kernel's select-based ring advance
 * XT_M_WAB=0     -> dedicated M-backward with the next K-tile's LDS writes before the
   closing barrier (default: after the opening one)
-* XT_W_TNG=2     -> dedicated rho-forward on 32-point blocks, two per CU
+* XT_W_TNG=2 / XT_W_XW=2 -> dedicated rho-forward on 32-point blocks / with two trial
+  pairs per wave (default: 64-point blocks of eight one-pair waves)
 * XT_XSF_FUSED=0 -> XSF Delta-A exchange as direct DF sandwiches
   (default with the stored exchange: one Kx stream for main + Delta-A exchange)
 * XT_SKINNY_RV=0 -> 33..40-row stored exchange through the 48-row MFMA tile
@@ -52,7 +53,9 @@ def env():
 
 @pytest.mark.parametrize("knobs", [dict(XT_M_KERNEL=0), dict(XT_W_KERNEL=0), dict(XT_M_KERNEL=0, XT_W_KERNEL=0),
                                    dict(XT_M_KERNEL=1, XT_W_KERNEL=1), dict(XT_W_RING=0),
-                                   dict(XT_M_WAB=0), dict(XT_W_KERNEL=1, XT_W_TNG=2)])
+                                   dict(XT_M_WAB=0), dict(XT_W_KERNEL=1, XT_W_TNG=2, XT_W_XW=2),
+                                   dict(XT_W_KERNEL=1, XT_W_TNG=2), dict(XT_W_KERNEL=1, XT_W_XW=2),
+                                   dict(XT_W_KERNEL=1, XT_W_TNG=2, XT_W_XW=2, XT_W_RING=0)])
 @pytest.mark.parametrize("nc,no,nao", [(5, 2, 26), (33, 1, 60), (35, 2, 70), (95, 2, 130), (99, 2, 140),
                                       (120, 3, 150)])
 def test_xc_kernel_variants(hiplib, env, knobs, nc, no, nao):

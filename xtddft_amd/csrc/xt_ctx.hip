@@ -1000,7 +1000,9 @@ static int xc_response(xt_ctx* c, int nz) {
       if (gga && w_ded && xc_rho_w_lds_bytes(O) <= 160 * 1024) {
         // dedicated kernel (xt_xcw.hip); tag 4 timing
         bool prof = false;
-        RET(prof_begin(c, 4, 2.0 * nzg * V * (double)n * O,
+        // flops: the T = PhiO^T Zp GEMM (2 O per T element) + the fused gradient
+        // contraction rhoW = sum_a dPhiV_c T (3 FMAs per T element)
+        RET(prof_begin(c, 4, 2.0 * nzg * V * (double)n * (O + 3),
                        8.0 * ((double)nzg * O * V + (double)n * O + 3.0 * n * V + 3.0 * n * nzg), &prof));
         const int r = xc_rho_w(O, nzg, V, n, PO, nmo, c->zp.p + gr[q].ch0 * chs, (long)nzg * V, V,
                                PV + compP, compP, nmo, Rg[q], ldR[q], c->st);
@@ -1015,7 +1017,7 @@ static int xc_response(xt_ctx* c, int nz) {
         f2.fz.w = PV + compP; f2.fz.wc = compP; f2.fz.wg = nmo;
         f2.fz.rho = Rg[q]; f2.fz.rg = ldR[q];
         f2.tag = 4;
-        f2.flops = 2.0 * nzg * V * (double)n * O;
+        f2.flops = 2.0 * nzg * V * (double)n * (O + 3);   // GEMM + fused contraction
         // Zp, PhiO0, dPhiV_{x,y,z} in; rhoW out
         f2.bytes = 8.0 * ((double)nzg * O * V + (double)n * O + 3.0 * n * V + 3.0 * n * nzg);
         RET(gemm(c, f2));
@@ -1051,7 +1053,9 @@ static int xc_response(xt_ctx* c, int nz) {
         if (O <= 128 && c->m_kernel) {
           // dedicated kernel (xt_xcm.hip); tag 5 timing around it and its reduce
           bool prof = false;
-          RET(prof_begin(c, 5, 2.0 * O * (double)nzg * V * n,
+          // flops: the PhiO^T M GEMM (2 O per M element) + generating M = sum_c wv_c
+          // dPhiV_c (3 FMAs per M element)
+          RET(prof_begin(c, 5, 2.0 * (O + 3) * (double)nzg * V * n,
                          8.0 * ((double)n * O + 3.0 * n * V + 3.0 * n * nzg + 2.0 * O * (double)nzg * V), &prof));
           const size_t need = xc_back_m_workspace_bytes(O, nzg, V, n);
           if (c->ws.n * sizeof(double) < need) RET(c->ws.ensure(need / sizeof(double) + 1));
@@ -1070,7 +1074,7 @@ static int xc_response(xt_ctx* c, int nz) {
         b2.fz.rho = Rg[q]; b2.fz.rg = ldR[q];
         b2.C = c->accT.p + gr[q].ch0 * chs; b2.ldc = (long)nzg * V; b2.beta = 1.0;
         b2.tag = 5;
-        b2.flops = 2.0 * O * (double)nzg * V * n;
+        b2.flops = 2.0 * (O + 3) * (double)nzg * V * n;   // GEMM + generated operand
         // PhiO0, dPhiV_{x,y,z}, wv in; accT read + written
         b2.bytes = 8.0 * ((double)n * O + 3.0 * n * V + 3.0 * n * nzg + 2.0 * O * (double)nzg * V);
         RET(gemm(c, b2));
