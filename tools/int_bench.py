@@ -3,13 +3,16 @@
 s/p/d "water" molecules (the basis of tests/test_gpu_qc.py::_spd_mol).
 python tools/int_bench.py [nmol ...]   (GPU needed for the device columns)"""
 import json
+import os
 import sys
 import time
 
 import numpy as np
 
-from xtddft_amd.qc import M
-from xtddft_amd.qc.df import aux_mole
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from xtddft_amd.qc import M  # noqa: E402
+from xtddft_amd.qc.df import aux_mole  # noqa: E402
 
 BASIS = {"O": [[0, [30.0, 0.3], [6.0, 0.7]], [0, [0.9, 1.0]], [1, [5.0, 0.4], [1.1, 0.7]], [2, [1.2, 1.0]]],
          "H": [[0, [3.0, 0.4], [0.5, 0.7]], [1, [0.8, 1.0]]]}
