@@ -59,7 +59,7 @@ __device__ __forceinline__ double rows4(double v) {
 // XW trial pairs per wave (WXB / XW waves per block, the block still covers WXB pairs):
 // XW = 2 runs one wave per SIMD with twice the accumulators (the MFMA accumulators in
 // AGPRs), each B fragment and weight read feeding both pairs.
-template <int TNG, bool BRANCHY, int XW = 1>
+template <int TNG, bool BRANCHY, int XW = 1, int ZDT = XCW_ZD>
 __global__ void __launch_bounds__(64 * WXB / XW)
 __attribute__((amdgpu_waves_per_eu(XW == 2 ? (TNG <= 2 ? 2 : 1) : (TNG <= 2 ? 4 : 2), XW == 2 ? (TNG <= 2 ? 2 : 1) : (TNG <= 2 ? 4 : 2))))
 k_xc_rho_w(int O, int nx, int V, int n,
@@ -68,6 +68,7 @@ k_xc_rho_w(int O, int nx, int V, int n,
            const double* __restrict__ Wg, long wc, long wg,
            double* __restrict__ Rout, long rg) {
   constexpr int GB = 16 * TNG;                 // grid points per block
+  constexpr int ZD = ZDT;                      // Zp ring depth (k-steps)
   constexpr int W_IMG = 3 * WA * GB;           // one weight buffer (doubles)
   constexpr int NT = 64 * WXB / XW;            // threads per block
   // XW = 2 stages each a-tile's weights in two halves (loaded before / stored after
@@ -325,25 +326,25 @@ static size_t rho_w_lds(int O, int tng) {
 
 size_t xc_rho_w_lds_bytes(int O) { return rho_w_lds(O, w_tng()); }
 
-template <int TNG, int XW = 1>
+template <int TNG, int XW = 1, int ZDT = XCW_ZD>
 static void launch_rho_w(int branchy, int blocks, size_t lds, hipStream_t st, int O, int nx, int V, int n,
                          const double* PO, long ldp, const double* Z, long zi, long zx, const double* W, long wc,
                          long wg, double* R, long rg) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_xc_rho_w<TNG, false, XW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_xc_rho_w<TNG, true, XW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_xc_rho_w<TNG, false, XW, ZDT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_xc_rho_w<TNG, true, XW, ZDT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   const int nt = 64 * WXB / XW;
   if (branchy)
-    hipLaunchKernelGGL((k_xc_rho_w<TNG, true, XW>), dim3(blocks), dim3(nt), lds, st, O, nx, V, n, PO, ldp, Z, zi,
-                       zx, W, wc, wg, R, rg);
+    hipLaunchKernelGGL((k_xc_rho_w<TNG, true, XW, ZDT>), dim3(blocks), dim3(nt), lds, st, O, nx, V, n, PO, ldp, Z,
+                       zi, zx, W, wc, wg, R, rg);
   else
-    hipLaunchKernelGGL((k_xc_rho_w<TNG, false, XW>), dim3(blocks), dim3(nt), lds, st, O, nx, V, n, PO, ldp, Z, zi,
-                       zx, W, wc, wg, R, rg);
+    hipLaunchKernelGGL((k_xc_rho_w<TNG, false, XW, ZDT>), dim3(blocks), dim3(nt), lds, st, O, nx, V, n, PO, ldp, Z,
+                       zi, zx, W, wc, wg, R, rg);
 }
 
 int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const double* Z, long zi, long zx,
@@ -364,6 +365,8 @@ int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const doub
     launch_rho_w<2>(branchy, blocks, lds, st, O, nx, V, n, PO, ldp, Z, zi, zx, W, wc, wg, R, rg);
   else if (w_xw() == 2)
     launch_rho_w<4, 2>(branchy, blocks, lds, st, O, nx, V, n, PO, ldp, Z, zi, zx, W, wc, wg, R, rg);
+  else if (getenv("XT_W_ZD") && atoi(getenv("XT_W_ZD")) == 6)   // a 6-k-step Zp ring
+    launch_rho_w<4, 1, 6>(branchy, blocks, lds, st, O, nx, V, n, PO, ldp, Z, zi, zx, W, wc, wg, R, rg);
   else
     launch_rho_w<4>(branchy, blocks, lds, st, O, nx, V, n, PO, ldp, Z, zi, zx, W, wc, wg, R, rg);
   return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
