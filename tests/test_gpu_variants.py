@@ -100,3 +100,20 @@ def test_stored_exchange_row_shapes(hiplib, env, nz, rv):
     z = make_trial_vectors(nz, hdiag.size)
     op = DeviceOperator(mf, "XTDA", k_mode="stored")
     assert rel(op.apply(z), vind(z)) < RTOL
+
+
+@pytest.mark.parametrize("kind,nz", [("XTDA", 1), ("XTDA", 8), ("XTDA", 9), ("XTDA", 16), ("SF_UP", 16),
+                                     ("SF_UP", 30)])
+def test_stored_exchange_small_row_counts(hiplib, kind, nz):
+    """The 16- and 32-row images of the streaming exchange kernel (M = 2 nz for X-TDA,
+    nz for SF-up: 2, 16 | 18, 32 | 16 | 30 rows) against the oracle."""
+    from oracle import sf_tda as osf
+    from xtddft_amd.operator import DeviceOperator
+    mf = make_mf(nao=40, nc=8, no=2, ngrid=2000, xctype="GGA", hyb=0.25)
+    if kind == "XTDA":
+        vind, hdiag = oxtda.gen_tda_operation(mf)
+    else:
+        vind, hdiag = osf.gen_tda_operation_sf(mf, isf=1)
+    z = make_trial_vectors(nz, hdiag.size)
+    op = DeviceOperator(mf, kind, k_mode="stored")
+    assert rel(op.apply(z), vind(z)) < RTOL

@@ -246,7 +246,15 @@ __global__ void k_skinny_transpose(int M, int K, int kslack, int MP, const doubl
 namespace {
 struct SkShape { int mp, bn, bk, slots; };
 // (padded rows, columns per block, k per chunk, concurrent blocks per CU)
+// The A image is as tall as the smallest MFMA row count that covers M (16 / 32 / 48):
+// a Davidson step with few new vectors streams Kx without the padded rows' MFMAs
+// (M = 2 nz <= 16 through 48 rows made the stream matrix-pipe bound).  M = 33..40
+// takes 32 MFMA rows + the VALU remainder rows (48-row image).
 SkShape sk_shape(int M) {
+  const char* e = getenv("XT_SKINNY_SMALL");   // 0: every M <= 48 through the 48-row image
+  const bool small = !(e && atoi(e) == 0);
+  if (small && M <= 16) return {16, 16 * 4 * SK_WAVES, 64, 2};
+  if (small && M <= 32) return {32, 16 * 4 * SK_WAVES, 64, 2};
   if (M <= 48) return {48, 16 * 4 * SK_WAVES, 64, 2};
   return {160, 16 * 2 * SK_WAVES, 32, 1};
 }
@@ -290,7 +298,13 @@ int skinny_gemm(int M, int N, int K, double alpha, const double* A, long lda, co
   const int used = (K + kchunk - 1) / kchunk;
   const char* erv = getenv("XT_SKINNY_RV");
   const bool rv = !(erv && atoi(erv) == 0) && M > 32 && M <= 40;
-  if (sh.mp == 48 && rv)
+  if (sh.mp == 16)
+    hipLaunchKernelGGL((k_skinny<1, 4, 64, 4>), dim3(strips, used), dim3(512), 0, st, N, K, kchunk, AT, B, ldb, part,
+                       (long)N);
+  else if (sh.mp == 32)
+    hipLaunchKernelGGL((k_skinny<2, 4, 64, 4>), dim3(strips, used), dim3(512), 0, st, N, K, kchunk, AT, B, ldb, part,
+                       (long)N);
+  else if (sh.mp == 48 && rv)
     hipLaunchKernelGGL((k_skinny<2, 4, 64, 4, 8>), dim3(strips, used), dim3(512), 0, st, N, K, kchunk, AT, B, ldb,
                        part, (long)N);
   else if (sh.mp == 48)
