@@ -23,3 +23,26 @@ def test_bench_self_launches_two_ranks():
     assert d["scaling"] == "strong" and d["value"] > 0
     assert d["verify"] < 1e-12, d["verify"]   # all-reduced shard sums == full operator
     assert "STUB" in d["data"]
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_the_gpu():
+    """The real operator at N = 2 (both ranks on the visible MI355X over gloo; the
+    driver's scaling run uses RCCL on separate GPUs): the launcher, grid / exchange-row
+    sharding per rank, the all-reduce of sigma and the max-over-ranks timing run end
+    to end and rank 0 prints one line (correctness of the shard sums:
+    test_gpu_parity.py::test_sharded_contexts_sum_to_full_operator)."""
+    env = dict(os.environ, XT_BENCH_BACKEND="gloo")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--nao", "120", "--nclosed", "20", "--nopen", "2", "--naux", "360", "--ngrid", "20000", "--nvec", "8",
+           "--no-cpu-baseline", "--no-converge"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and "STUB" not in d["data"]
+    assert "grid sharded x2" in d["config"]["parallelism"]
