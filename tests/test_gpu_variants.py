@@ -56,7 +56,7 @@ def env():
                                    dict(XT_M_WAB=0), dict(XT_W_KERNEL=1, XT_W_TNG=2, XT_W_XW=2),
                                    dict(XT_W_KERNEL=1, XT_W_TNG=2), dict(XT_W_KERNEL=1, XT_W_XW=2),
                                    dict(XT_W_KERNEL=1, XT_W_TNG=2, XT_W_XW=2, XT_W_RING=0),
-                                   dict(XT_W_KERNEL=1, XT_W_ZD=6)])
+                                   dict(XT_W_KERNEL=1, XT_W_ZD=6), dict(XT_W_KERNEL=1, XT_W_ORDER=1)])
 @pytest.mark.parametrize("nc,no,nao", [(5, 2, 26), (33, 1, 60), (35, 2, 70), (95, 2, 130), (99, 2, 140),
                                       (120, 3, 150)])
 def test_xc_kernel_variants(hiplib, env, knobs, nc, no, nao):

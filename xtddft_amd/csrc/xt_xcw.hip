@@ -66,7 +66,7 @@ k_xc_rho_w(int O, int nx, int V, int n,
            const double* __restrict__ PO, long ldp,
            const double* __restrict__ Z, long zi, long zx,
            const double* __restrict__ Wg, long wc, long wg,
-           double* __restrict__ Rout, long rg) {
+           double* __restrict__ Rout, long rg, int xs_fast) {
   constexpr int GB = 16 * TNG;                 // grid points per block
   constexpr int ZD = ZDT;                      // Zp ring depth (k-steps)
   constexpr int W_IMG = 3 * WA * GB;           // one weight buffer (doubles)
@@ -94,7 +94,10 @@ k_xc_rho_w(int O, int nx, int V, int n,
     const int xcd = lid & 7, idx = lid >> 3, qn = nblk >> 3, rem = nblk & 7;
     lid = xcd * qn + (xcd < rem ? xcd : rem) + idx;
   }
-  const int gt = lid % ntg, xs = lid / ntg;
+  // xs_fast (XT_W_ORDER=1): the trial-pair sets of one g-tile side by side instead (they
+  // share the g-tile's gradient weights in L2; the Zp slices then come from MALL)
+  const int nxs = (nx + WXB - 1) / WXB;
+  const int gt = xs_fast ? lid / nxs : lid % ntg, xs = xs_fast ? lid % nxs : lid / ntg;
   const int g0 = gt * GB, x0 = xs * WXB;
   const int xg = x0 + wave * XW;               // this wave's first trial pair
   const bool wave_on = xg < nx;
@@ -314,6 +317,11 @@ static int w_tng() {
   return e && atoi(e) == 2 ? 2 : 4;
 }
 
+static int w_order() {                         // XT_W_ORDER=1: trial-pair sets fastest
+  const char* e = getenv("XT_W_ORDER");
+  return e && atoi(e) == 1 ? 1 : 0;
+}
+
 static int w_xw() {
   const char* e = getenv("XT_W_XW");
   return e && atoi(e) == 2 ? 2 : 1;
@@ -341,10 +349,10 @@ static void launch_rho_w(int branchy, int blocks, size_t lds, hipStream_t st, in
   const int nt = 64 * WXB / XW;
   if (branchy)
     hipLaunchKernelGGL((k_xc_rho_w<TNG, true, XW, ZDT>), dim3(blocks), dim3(nt), lds, st, O, nx, V, n, PO, ldp, Z,
-                       zi, zx, W, wc, wg, R, rg);
+                       zi, zx, W, wc, wg, R, rg, w_order());
   else
     hipLaunchKernelGGL((k_xc_rho_w<TNG, false, XW, ZDT>), dim3(blocks), dim3(nt), lds, st, O, nx, V, n, PO, ldp, Z,
-                       zi, zx, W, wc, wg, R, rg);
+                       zi, zx, W, wc, wg, R, rg, w_order());
 }
 
 int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const double* Z, long zi, long zx,
