@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define XT_ABI_VERSION 3
+#define XT_ABI_VERSION 4
 
 #define XT_PTR_HOST 0
 #define XT_PTR_DEVICE 1
@@ -190,10 +190,12 @@ int xt_row_scale(int nrow, int dim, double* x, const double* s, void* hip_stream
    The ket may be a shell pair (4-index (ab|cd), the stored-ERI path of `jk_mode`
    ERI8 / PySCF mol.intor('int2e')): lc = l_c + l_d, nc = ncart(l_c) ncart(l_d),
    its primitive pairs in aux_prim and its pair Hermite coefficients in ek.
-   lmax_orb <= 2, lmax_aux <= 6 (the ket's Hermite order). */
+   lmax_orb <= 2, lmax_aux <= 6 (the ket's Hermite order).  omega > 0: the long-range
+   operator erf(omega r12)/r12 (PySCF mol.with_range_coulomb, the cderi_lr / eri_lr
+   factors of range-separated hybrids, XTDA.py:501,527-539); 0: 1/r12. */
 int xt_int3c2e_cart(int npair, const int* pair_info, const double* pair_prim, const double* eab,
                     int naux_shells, const int* aux_info, const double* aux_prim, const double* ek,
-                    int lmax_orb, int lmax_aux, double* out, long ldo, void* hip_stream);
+                    int lmax_orb, int lmax_aux, double omega, double* out, long ldo, void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -69,19 +69,21 @@ def _spd_mol():
     return M(atoms, basis=basis, unit="Bohr")
 
 
+@pytest.mark.parametrize("omega", [0.0, 0.33])
 @pytest.mark.parametrize("which", ["hf_631g", "spd"])
-def test_device_int3c2e_equals_host(torch, which):
+def test_device_int3c2e_equals_host(torch, which, omega):
     """The HIP 3-index integrals (csrc/xt_int.hip) against the host McMurchie-Davidson
     routine (qc/ints.py eri3c, itself checked against the 4-index routine):
     HF / 6-31G with its even-tempered auxiliary basis (aux l <= 3) and an s/p/d
     molecule (aux l <= 5; exponents up to 30 put the Boys argument on both sides of
     the series / asymptotic switch at T = 30).  Tolerance 1e-12 of the largest
-    integral (FP64 round-off of a different summation order)."""
+    integral (FP64 round-off of a different summation order).  omega = 0.33: the
+    long-range operator erf(omega r12)/r12."""
     from xtddft_amd.qc.df import aux_mole
     mol = hf_mol() if which == "hf_631g" else _spd_mol()
     aux = aux_mole(mol)
-    host = mol.int3c2e(aux)
-    dev = mol.int3c2e(aux, device=0)
+    host = mol.int3c2e(aux, omega=omega)
+    dev = mol.int3c2e(aux, device=0, omega=omega)
     assert dev.shape == host.shape
     assert np.abs(dev - host).max() < 1e-12 * np.abs(host).max()
 
@@ -95,13 +97,14 @@ def test_density_fitted_scf_with_device_integrals(torch):
     assert abs(dev.e_tot - host.e_tot) < 1e-10
 
 
+@pytest.mark.parametrize("omega", [0.0, 0.33])
 @pytest.mark.parametrize("which", ["hf_631g", "spd"])
-def test_device_eri_full_equals_host(torch, which):
+def test_device_eri_full_equals_host(torch, which, omega):
     """The 4-index ERIs through the same HIP kernel with the ket given as shell pairs
     (ket Hermite order up to 4, L <= 8) against the host routine, all 8 symmetry
     copies; tolerance 1e-12 of the largest integral."""
     mol = hf_mol() if which == "hf_631g" else _spd_mol()
-    host = mol.eri_full()
-    dev = mol.eri_full(device=0)
+    host = mol.eri_full(omega=omega)
+    dev = mol.eri_full(device=0, omega=omega)
     assert np.abs(dev - host).max() < 1e-12 * np.abs(host).max()
     assert np.abs(dev - dev.transpose(2, 3, 0, 1)).max() == 0.0

@@ -27,7 +27,7 @@ def test_library_builds_and_exports_every_header_symbol(hiplib):
     assert len(syms) >= 20
     for s in syms:
         assert hasattr(hiplib, s), s
-    assert hiplib.xt_abi_version() == 3
+    assert hiplib.xt_abi_version() == 4
 
 
 def test_desc_layout_matches_c_header(tmp_path):

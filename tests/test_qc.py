@@ -318,3 +318,25 @@ def test_density_fitted_scf():
     assert abs(mf.e_tot - reference_outputs()["roks_bhandhlyp_e_tot"]) < 1e-5
     m = mf.to_meanfield()
     assert m.jk_mode == "DF" and m.eri is None and m.naux == b.shape[0]
+
+
+def test_long_range_coulomb_integrals_limits_and_df():
+    """erf(omega r12)/r12 integrals (the range-separated exchange factors): the full
+    Coulomb ERIs as omega -> infinity; (2 omega / sqrt(pi)) S_ab S_cd as omega -> 0
+    (erf(w r)/r = 2w/sqrt(pi) (1 - w^2 r^2 / 3 + ...)); and the long-range DF factor
+    (3- and 2-index integrals both attenuated) reproduces the long-range ERIs within
+    the fitting error of the Coulomb factor."""
+    from molecules import hf_mol
+    from xtddft_amd.qc.df import DF
+    mol = hf_mol()
+    full = mol.eri_full()
+    big = mol.eri_full(omega=1e4)
+    assert np.abs(big - full).max() < 1e-6 * np.abs(full).max()
+    w = 1e-4
+    s = mol.intor("int1e_ovlp")
+    small = mol.eri_full(omega=w) / (2 * w / np.sqrt(np.pi))
+    ref = np.einsum('ij,kl->ijkl', s, s)
+    assert np.abs(small - ref).max() < 1e-6 * np.abs(ref).max()
+    lr = mol.eri_full(omega=0.33)
+    b = DF(mol).build().cderi_lr(0.33)
+    assert np.abs(np.einsum('pij,pkl->ijkl', b, b) - lr).max() < 5e-4

@@ -43,7 +43,7 @@ class XtDesc(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 3   # include/xtddft_amd.h XT_ABI_VERSION
+ABI_VERSION = 4   # include/xtddft_amd.h XT_ABI_VERSION
 
 
 class LibraryMissing(RuntimeError):
@@ -101,7 +101,7 @@ def lib():
     L.xt_precond.argtypes = [c_int, c_int, dp, dp, c_double, dp, dp, vp]
     L.xt_row_norms2.argtypes = [c_int, c_int, dp, dp, vp]
     L.xt_row_scale.argtypes = [c_int, c_int, dp, dp, vp]
-    L.xt_int3c2e_cart.argtypes = [c_int, vp, dp, dp, c_int, vp, dp, dp, c_int, c_int, dp, c_long, vp]
+    L.xt_int3c2e_cart.argtypes = [c_int, vp, dp, dp, c_int, vp, dp, dp, c_int, c_int, c_double, dp, c_long, vp]
     for name in EXPORTS:
         if not hasattr(L, name):
             raise LibraryMissing(f"{LIB_PATH} lacks symbol {name}")

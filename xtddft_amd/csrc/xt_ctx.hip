@@ -1391,11 +1391,13 @@ extern "C" int xt_row_scale(int nrow, int dim, double* x, const double* s, void*
 
 extern "C" int xt_int3c2e_cart(int npair, const int* pair_info, const double* pair_prim, const double* eab,
                                int naux_shells, const int* aux_info, const double* aux_prim, const double* ek,
-                               int lmax_orb, int lmax_aux, double* out, long ldo, void* stream) {
+                               int lmax_orb, int lmax_aux, double omega, double* out, long ldo,
+                               void* stream) {
   if (npair < 0 || naux_shells < 0 || ldo < 0) return fail(XT_ERR_ARG, "xt_int3c2e_cart: negative size");
   if (lmax_orb > kInt3cMaxLab || lmax_aux > kInt3cMaxLc)
     return fail(XT_ERR_ARG, "xt_int3c2e_cart: orbital shells up to d and auxiliary shells up to l = 6");
+  if (omega < 0.0) return fail(XT_ERR_ARG, "xt_int3c2e_cart: omega < 0");
   const int r = int3c2e_cart(npair, pair_info, pair_prim, eab, naux_shells, aux_info, aux_prim, ek, out, ldo,
-                             (hipStream_t)stream);
+                             omega, (hipStream_t)stream);
   return r ? fail(r, "int3c2e launch failed") : 0;
 }

@@ -12,6 +12,8 @@
 // the quartic part -- Boys functions, the Hermite integrals R_tuv by the downward
 // recursion, and the two contractions -- one thread per (shell pair, aux shell),
 // the R table in private memory.  Not a hot-path kernel (once per mean field).
+// omega > 0 evaluates the long-range operator erf(omega r12)/r12 instead (the
+// range-separated exchange factors; qc/ints.py _attenuate).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include "xt_internal.h"
@@ -99,7 +101,7 @@ __global__ void __launch_bounds__(64)
 k_int3c2e_cart(int npair, const int* __restrict__ pair_info, const double* __restrict__ pair_prim,
                const double* __restrict__ eab, int naux, const int* __restrict__ aux_info,
                const double* __restrict__ aux_prim, const double* __restrict__ ek,
-               double* __restrict__ out, long ldo) {
+               double* __restrict__ out, long ldo, double omega) {
   const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= (long)npair * naux) return;
   const int k = (int)(id / naux), j = (int)(id % naux);
@@ -116,9 +118,14 @@ k_int3c2e_cart(int npair, const int* __restrict__ pair_info, const double* __res
     for (int r = 0; r < nr; ++r) {
       const double* cp = aux_prim + 4 * (long)(ar0 + r);
       const double s = cp[0];
-      const double alpha = p * s / (p + s);
+      double alpha = p * s / (p + s), scale = 1.0;
+      if (omega > 0.0) {   // erf(omega r)/r: 1/a' = 1/alpha + 1/omega^2, times sqrt(a'/alpha)
+        const double w2 = omega * omega, a2 = alpha * w2 / (alpha + w2);
+        scale = sqrt(a2 / alpha);
+        alpha = a2;
+      }
       hermite_r(L, alpha, pp[1] - cp[1], pp[2] - cp[2], pp[3] - cp[3], R, S);
-      const double pref = 2.0 * pow(M_PI, 2.5) / (p * s * sqrt(p + s));
+      const double pref = 2.0 * pow(M_PI, 2.5) / (p * s * sqrt(p + s)) * scale;
       for (int c = 0; c < nc; ++c) {
         // M[t] = sum_u (-1)^{|u|} E^c_u(r) R[t + u]
         const double* e = ek + ae0 + ((long)c * ntc) * nr + r;
@@ -149,12 +156,12 @@ k_int3c2e_cart(int npair, const int* __restrict__ pair_info, const double* __res
 
 int int3c2e_cart(int npair, const int* pair_info, const double* pair_prim, const double* eab, int naux_shells,
                  const int* aux_info, const double* aux_prim, const double* ek, double* out, long ldo,
-                 hipStream_t st) {
+                 double omega, hipStream_t st) {
   const long n = (long)npair * naux_shells;
   if (n == 0) return 0;
   const int blk = 64;
   hipLaunchKernelGGL(k_int3c2e_cart, dim3((unsigned)((n + blk - 1) / blk)), dim3(blk), 0, st, npair, pair_info,
-                     pair_prim, eab, naux_shells, aux_info, aux_prim, ek, out, ldo);
+                     pair_prim, eab, naux_shells, aux_info, aux_prim, ek, out, ldo, omega);
   return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
 }
 

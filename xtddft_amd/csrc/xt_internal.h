@@ -92,7 +92,7 @@ size_t xc_rho_w_lds_bytes(int O);
 constexpr int kInt3cMaxLab = 2, kInt3cMaxLc = 6;
 int int3c2e_cart(int npair, const int* pair_info, const double* pair_prim, const double* eab, int naux_shells,
                  const int* aux_info, const double* aux_prim, const double* ek, double* out, long ldo,
-                 hipStream_t st);
+                 double omega, hipStream_t st);
 int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const double* Z, long zi, long zx,
              const double* W, long wc, long wg, double* R, long rg, hipStream_t st);
 size_t dgemm_workspace_bytes(const GemmDesc& d);

@@ -111,6 +111,14 @@ class DF:
     def cderi(self):
         return self.build()._cderi
 
+    def cderi_lr(self, omega: float):
+        """The long-range factor of erf(omega r12)/r12 (PySCF ``with_df.range_coulomb``:
+        3-index and 2-index integrals both attenuated), the ``cderi_lr`` of a
+        range-separated mean field (MeanField, XTDA.py:527-539)."""
+        self.build()
+        j3 = self.mol.int3c2e(self.auxmol, device=self.device, omega=omega)
+        return cholesky_cderi(j3, self.auxmol.int2c2e(omega=omega))
+
     def get_jk(self, dms, with_j=True, with_k=True):
         """J[D] = sum_P B_P <B_P, D>, K[D] = sum_P B_P D B_P (PySCF convention)."""
         b = self.cderi

@@ -41,8 +41,9 @@ def _block_transform(shells):
     return T
 
 
-def int3c2e_device(mol, auxmol, device: int = 0):
-    """(P|mu nu) over normalised spherical functions, (naux, nao, nao), on the GPU."""
+def int3c2e_device(mol, auxmol, device: int = 0, omega: float = 0.0):
+    """(P|mu nu) over normalised spherical functions, (naux, nao, nao), on the GPU
+    (omega > 0: erf(omega r12)/r12)."""
     import torch
     L = _capi.lib()
     dev = torch.device(f"cuda:{device}")
@@ -73,8 +74,8 @@ def int3c2e_device(mol, auxmol, device: int = 0):
         st = torch.cuda.current_stream(dev).cuda_stream
         _capi.check(L.xt_int3c2e_cart(len(prow), t_pinfo.data_ptr(), t_pprim.data_ptr(), t_eab.data_ptr(),
                                       len(ash), t_ainfo.data_ptr(), t_aprim.data_ptr(), t_ek.data_ptr(),
-                                      max(s.l for s in sh), max(s.l for s in ash), cart.data_ptr(), ncol,
-                                      ctypes.c_void_p(st)), "xt_int3c2e_cart")
+                                      max(s.l for s in sh), max(s.l for s in ash), float(omega), cart.data_ptr(),
+                                      ncol, ctypes.c_void_p(st)), "xt_int3c2e_cart")
         # spherical on both sides (pair blocks Ti (x) Tj, aux blocks Ta), then the
         # (mu nu) fill as one gather of pair rows
         ysph = _mm(L, st, dev, _mm(L, st, dev, dt(tp), cart), dt(_block_transform(ash)), tb=1)   # (npair_sph, naux)
@@ -137,7 +138,7 @@ def _pairs(mol):
     return np.array(pinfo, dtype=np.int32), np.concatenate(pprim), np.concatenate(eab), prow, row
 
 
-def eri_full_device(mol, device: int = 0):
+def eri_full_device(mol, device: int = 0, omega: float = 0.0):
     """(mu nu|la si) over normalised spherical AOs, all 8 symmetry copies (as
     ``Mole.eri_full``, PySCF ``mol.intor('int2e')``), on the GPU: the bra and the
     ket are the same shell-pair tables, the Cartesian (pair x pair) matrix comes
@@ -165,7 +166,7 @@ def eri_full_device(mol, device: int = 0):
         st = torch.cuda.current_stream(dev).cuda_stream
         _capi.check(L.xt_int3c2e_cart(len(prow), t_pinfo.data_ptr(), t_pprim.data_ptr(), t_eab.data_ptr(),
                                       len(prow), t_ainfo.data_ptr(), t_pprim.data_ptr(), t_eab.data_ptr(),
-                                      lmax, 2 * lmax, cart.data_ptr(), ncart_tot, ctypes.c_void_p(st)),
+                                      lmax, 2 * lmax, float(omega), cart.data_ptr(), ncart_tot, ctypes.c_void_p(st)),
                     "xt_int3c2e_cart (4-index)")
         t_tp = dt(tp)
         s_ = _mm(L, st, dev, _mm(L, st, dev, t_tp, cart), t_tp, tb=1)          # (nsph_tot, nsph_tot)

@@ -282,13 +282,15 @@ class Mole:
         return {l: (AuxShellSet([self.shells[k] for k in ks]), [int(self.ao_loc[k]) for k in ks])
                 for l, ks in groups.items()}
 
-    def int3c2e(self, auxmol, device=None) -> np.ndarray:
+    def int3c2e(self, auxmol, device=None, omega: float = 0.0) -> np.ndarray:
         """(P|mu nu) over normalised spherical functions: (naux, nao, nao) -- PySCF
         ``df.incore.aux_e2(mol, auxmol, 'int3c2e')`` transposed to aux-major.
-        ``device=k``: evaluated on GPU k (``qc.dints``, the HIP integral kernel)."""
+        ``device=k``: evaluated on GPU k (``qc.dints``, the HIP integral kernel);
+        ``omega > 0``: the long-range operator erf(omega r12)/r12 (PySCF
+        ``mol.with_range_coulomb(omega)``)."""
         if device is not None:
             from .dints import int3c2e_device
-            return int3c2e_device(self, auxmol, device)
+            return int3c2e_device(self, auxmol, device, omega=omega)
         n, naux = self._nao, auxmol.nao
         out = np.zeros((naux, n, n))
         aux = auxmol._aux_groups()
@@ -302,7 +304,7 @@ class Mole:
                 b = slice(self.ao_loc[j], self.ao_loc[j + 1])
                 pair = ShellPair(sh[i], sh[j])
                 for l, (aset, offs) in aux.items():
-                    blk = eri3c(pair, aset)                          # (ca, cb, k, cP)
+                    blk = eri3c(pair, aset, omega)                   # (ca, cb, k, cP)
                     blk = np.einsum('mi,nj,ijkc,pc->kpmn', Ti, Tj, blk, Ta[l], optimize=True)
                     for k, o in enumerate(offs):
                         out[o:o + 2 * l + 1, a, b] = blk[k]
@@ -311,14 +313,15 @@ class Mole:
         out *= auxmol._norm[:, None, None] * nrm[None, :, None] * nrm[None, None, :]
         return out
 
-    def int2c2e(self) -> np.ndarray:
-        """(P|Q) of this (auxiliary) basis over normalised spherical functions."""
+    def int2c2e(self, omega: float = 0.0) -> np.ndarray:
+        """(P|Q) of this (auxiliary) basis over normalised spherical functions
+        (omega > 0: erf(omega r12)/r12)."""
         n = self._nao
         out = np.zeros((n, n))
         groups = self._aux_groups()
         for la, (sa, oa) in groups.items():
             for lb, (sb, ob) in groups.items():
-                blk = eri2c(sa, sb)                                  # (ka, ca, kb, cb)
+                blk = eri2c(sa, sb, omega)                           # (ka, ca, kb, cb)
                 blk = np.einsum('pa,kalc,qc->kplq', _sph_transform(la), blk, _sph_transform(lb),
                                 optimize=True)
                 for k, o1 in enumerate(oa):
@@ -327,12 +330,13 @@ class Mole:
         nrm = self._norm
         return out * (nrm[:, None] * nrm[None, :])
 
-    def eri_full(self, device=None) -> np.ndarray:
+    def eri_full(self, device=None, omega: float = 0.0) -> np.ndarray:
         """(mu nu|la si) over normalised spherical AOs, all 8 symmetry copies filled.
-        ``device=k``: evaluated on GPU k (``qc.dints``, the HIP integral kernel)."""
+        ``device=k``: evaluated on GPU k (``qc.dints``, the HIP integral kernel);
+        ``omega > 0``: erf(omega r12)/r12 (the long-range ERIs of ``eri_lr``)."""
         if device is not None:
             from .dints import eri_full_device
-            return eri_full_device(self, device)
+            return eri_full_device(self, device, omega=omega)
         n = self._nao
         sh = self.shells
         nsh = len(sh)
@@ -347,7 +351,7 @@ class Mole:
             bra = pairs[(i, j)]
             for (k, l) in keys[:ij + 1]:
                 ket = pairs[(k, l)]
-                blk = eri_quartet(bra, ket)
+                blk = eri_quartet(bra, ket, omega)
                 blk = np.einsum('ai,bj,ijkl,ck,dl->abcd', T[i], T[j], blk, T[k], T[l], optimize=True)
                 a = slice(self.ao_loc[i], self.ao_loc[i + 1])
                 b = slice(self.ao_loc[j], self.ao_loc[j + 1])

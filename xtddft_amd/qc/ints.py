@@ -144,6 +144,18 @@ def hermite_r(L: int, alpha: np.ndarray, X: np.ndarray, Y: np.ndarray, Z: np.nda
     return np.stack([prev[k] for k in tuv])
 
 
+def _attenuate(alpha, omega):
+    """erf(omega r)/r instead of 1/r: the Hermite integrals of the attenuated operator
+    are sqrt(a'/alpha) R_tuv(a') with 1/a' = 1/alpha + 1/omega^2 (the Fourier factor
+    exp(-k^2 / 4 omega^2) folded into the Gaussian product's exponent).  Returns
+    (exponent for R, prefactor scale); omega = 0 is the full Coulomb operator."""
+    if not omega:
+        return alpha, 1.0
+    w2 = omega * omega
+    a2 = alpha * w2 / (alpha + w2)
+    return a2, np.sqrt(a2 / alpha)
+
+
 # ------------------------------------------------------------ shell pairs
 class ShellPair:
     """Primitive-pair data of two contracted Cartesian shells (A, B).
@@ -292,15 +304,16 @@ class ShellPair:
         return acc
 
 
-def eri_quartet(bra: ShellPair, ket: ShellPair) -> np.ndarray:
-    """(ab|cd) over Cartesian components: (nca, ncb, ncc, ncd)."""
+def eri_quartet(bra: ShellPair, ket: ShellPair, omega: float = 0.0) -> np.ndarray:
+    """(ab|cd) over Cartesian components: (nca, ncb, ncc, ncd); omega > 0: the
+    long-range operator erf(omega r12)/r12."""
     p = bra.p[:, None]
     q = ket.p[None, :]
-    alpha = p * q / (p + q)
+    alpha, scale = _attenuate(p * q / (p + q), omega)
     d = bra.P[:, None, :] - ket.P[None, :, :]
     L = bra.L + ket.L
     R = hermite_r(L, alpha, d[..., 0], d[..., 1], d[..., 2])          # (ntuv_L, P, Q)
-    pref = 2.0 * np.pi ** 2.5 / (p * q * np.sqrt(p + q))
+    pref = 2.0 * np.pi ** 2.5 / (p * q * np.sqrt(p + q)) * scale
     idx, sign = _sum_table(bra.L, ket.L)
     Rm = R[idx] * pref                                                 # (ntab, ntcd, P, Q)
     X = np.einsum('tsPQ,s,cdsQ->tcdP', Rm, sign, ket.Eab, optimize=True)
@@ -341,16 +354,16 @@ class AuxShellSet:
         self.Ek = Ek
 
 
-def eri3c(bra: ShellPair, aux: AuxShellSet) -> np.ndarray:
+def eri3c(bra: ShellPair, aux: AuxShellSet, omega: float = 0.0) -> np.ndarray:
     """(ab|P) over Cartesian components for every shell of ``aux``:
-    (nca, ncb, nshell_aux, ncart_aux)."""
+    (nca, ncb, nshell_aux, ncart_aux); omega > 0: erf(omega r12)/r12."""
     p = bra.p[:, None]
     q = aux.p[None, :]
-    alpha = p * q / (p + q)
+    alpha, scale = _attenuate(p * q / (p + q), omega)
     d = bra.P[:, None, :] - aux.P[None, :, :]
     L = bra.L + aux.l
     R = hermite_r(L, alpha, d[..., 0], d[..., 1], d[..., 2])          # (ntuv_L, P, Q)
-    pref = 2.0 * np.pi ** 2.5 / (p * q * np.sqrt(p + q))
+    pref = 2.0 * np.pi ** 2.5 / (p * q * np.sqrt(p + q)) * scale
     idx, sign = _sum_table(bra.L, aux.l)
     Rm = R[idx] * pref                                                 # (ntab, ntc, P, Q)
     X = np.einsum('tsPQ,s,csQ->tcPQ', Rm, sign, aux.Ek, optimize=True)
@@ -358,15 +371,16 @@ def eri3c(bra: ShellPair, aux: AuxShellSet) -> np.ndarray:
     return np.einsum('abtP,tcPk->abkc', bra.Eab, X, optimize=True)
 
 
-def eri2c(auxa: AuxShellSet, auxb: AuxShellSet) -> np.ndarray:
-    """(P|Q) over Cartesian components: (nshell_a, nca, nshell_b, ncb)."""
+def eri2c(auxa: AuxShellSet, auxb: AuxShellSet, omega: float = 0.0) -> np.ndarray:
+    """(P|Q) over Cartesian components: (nshell_a, nca, nshell_b, ncb); omega > 0:
+    erf(omega r12)/r12."""
     p = auxa.p[:, None]
     q = auxb.p[None, :]
-    alpha = p * q / (p + q)
+    alpha, scale = _attenuate(p * q / (p + q), omega)
     d = auxa.P[:, None, :] - auxb.P[None, :, :]
     L = auxa.l + auxb.l
     R = hermite_r(L, alpha, d[..., 0], d[..., 1], d[..., 2])
-    pref = 2.0 * np.pi ** 2.5 / (p * q * np.sqrt(p + q))
+    pref = 2.0 * np.pi ** 2.5 / (p * q * np.sqrt(p + q)) * scale
     idx, sign = _sum_table(auxa.l, auxb.l)
     Rm = R[idx] * pref
     X = np.einsum('tsPQ,s,csQ->tcPQ', Rm, sign, auxb.Ek, optimize=True) @ auxb.seg   # (nta, ncb, Pprim, kb)
