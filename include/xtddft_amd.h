@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define XT_ABI_VERSION 4
+#define XT_ABI_VERSION 5
 
 #define XT_PTR_HOST 0
 #define XT_PTR_DEVICE 1
@@ -190,12 +190,37 @@ int xt_row_scale(int nrow, int dim, double* x, const double* s, void* hip_stream
    The ket may be a shell pair (4-index (ab|cd), the stored-ERI path of `jk_mode`
    ERI8 / PySCF mol.intor('int2e')): lc = l_c + l_d, nc = ncart(l_c) ncart(l_d),
    its primitive pairs in aux_prim and its pair Hermite coefficients in ek.
-   lmax_orb <= 2, lmax_aux <= 6 (the ket's Hermite order).  omega > 0: the long-range
-   operator erf(omega r12)/r12 (PySCF mol.with_range_coulomb, the cderi_lr / eri_lr
-   factors of range-separated hybrids, XTDA.py:501,527-539); 0: 1/r12. */
+   lmax_orb <= 3 (f), 2 lmax_orb + lmax_aux <= 13 (lmax_aux: the ket's Hermite order).
+   omega > 0: the long-range operator erf(omega r12)/r12 (PySCF mol.with_range_coulomb,
+   the cderi_lr / eri_lr factors of range-separated hybrids, XTDA.py:501,527-539); 0: 1/r12. */
 int xt_int3c2e_cart(int npair, const int* pair_info, const double* pair_prim, const double* eab,
                     int naux_shells, const int* aux_info, const double* aux_prim, const double* ek,
                     int lmax_orb, int lmax_aux, double omega, double* out, long ldo, void* hip_stream);
+/* The same integrals with Schwarz screening and a diagonal mode -- the exact ERIs of
+   the direct-SCF mean field (PySCF's default mf, whose get_jk XTDA.py:518-543 calls
+   and whose ERIs ao2mo.general transforms, XTDA.py:120) without the 4-index array:
+   the integral-direct pivoted Cholesky of xtddft_amd/qc/dchol.py evaluates the
+   diagonal (ab|ab) (diag = 1: one block per bra pair with ket = the same table
+   entry, nket == npair) and the pivot columns (all pairs | chosen pairs) through it.
+   q_bra / q_ket (device, per table entry; both or neither): blocks with
+   q_bra[k] q_ket[j] < q_thr are skipped (left zero). */
+int xt_int2e_cart(int npair, const int* pair_info, const double* pair_prim, const double* eab,
+                  int nket, const int* ket_info, const double* ket_prim, const double* ek,
+                  int lmax_orb, int lket, double omega, const double* q_bra, const double* q_ket,
+                  double q_thr, int diag, double* out, long ldo, void* hip_stream);
+/* AO values (deriv 0) or values and gradients (deriv 1) of normalised spherical
+   AOs on grid points (PySCF mol.eval_ao / ni.block_loop, SF_TDA.py:63-68, the AO
+   input of cache_xc_kernel / nr_uks_fxc, XTDA.py:504,514), device pointers:
+     coords[3g + 0..2]      grid point (Bohr)
+     shell_info[8s + 0..3]  l (<= 4), nprim, offset in shell_data, first AO
+     shell_data[off ..]     nprim exponents, nprim coefficients (x radial norms), centre
+     sph                    solid-harmonic tables of l = 0..4 ((2l+1) x ncart(l) each,
+                            concatenated, libcint order)
+     ao_norm[ao]            AO normalisation
+     out[c * comp_stride + g * ldo + ao], c = value (, d/dx, d/dy, d/dz). */
+int xt_eval_ao(int ngrid, const double* coords, int nshell, const int* shell_info,
+               const double* shell_data, const double* sph, const double* ao_norm, int deriv,
+               double* out, long ldo, long comp_stride, void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -88,3 +88,27 @@ def fd_xc_response(scf, mfield, z, eps=1e-5):
         out[x] = np.concatenate([np.einsum('pq,qo,pv->ov', v1[s], co, cv).ravel()
                                  for s, (co, cv) in enumerate(blocks)])
     return out
+
+
+HF_POL_BASIS = None
+
+
+def hf_pol_basis():
+    """6-31G (the reference's embedded F / H data) plus synthetic polarisation on F:
+    one d (exponent 1.4) and one f (exponent 1.0) -- an s/p/d/f basis for the
+    front-end tests (no def2 data can be loaded offline)."""
+    from xtddft_amd.qc.basis import _631G
+    return {"F": list(_631G["F"]) + [[2, [1.4, 1.0]], [3, [1.0, 1.0]]], "H": list(_631G["H"])}
+
+
+def hf_cluster(n: int, charge: int = 1, spin: int = 1, spacing: float = 2.9):
+    """(HF)_n on a 3 x 3 x k lattice (Angstrom), bond 0.917 A, H pointing along a
+    site-dependent axis (no symmetry): 23 AOs per HF in ``hf_pol_basis``."""
+    import numpy as np
+    axes = np.array([[0, 0, 1], [1, 0, 0], [0, 1, 0], [0.6, 0.8, 0], [0, -0.6, 0.8], [-0.8, 0, 0.6]])
+    atoms = []
+    for i in range(n):
+        site = np.array([i % 3, (i // 3) % 3, i // 9], dtype=float) * spacing
+        atoms.append(("F", tuple(site)))
+        atoms.append(("H", tuple(site + 0.917 * axes[i % len(axes)])))
+    return M(atoms, basis=hf_pol_basis(), charge=charge, spin=spin)

@@ -340,3 +340,49 @@ def test_long_range_coulomb_integrals_limits_and_df():
     lr = mol.eri_full(omega=0.33)
     b = DF(mol).build().cderi_lr(0.33)
     assert np.abs(np.einsum('pij,pkl->ijkl', b, b) - lr).max() < 5e-4
+
+
+def test_pair_table_index_maps():
+    """qc.dints.PairTable (host side of the device integral path): the spherical
+    pair rows, the packed index mu (mu+1)/2 + nu and the block-sparse transform
+    classes cover every AO pair exactly once (s/p/d/f basis)."""
+    from xtddft_amd.qc import M
+    from xtddft_amd.qc.dints import PairTable
+    from molecules import hf_pol_basis
+    mol = M("F 0 0 0; H 0.3 0.2 0.917; H -0.6 0.1 -0.5", basis=hf_pol_basis(), charge=1, spin=0)
+    tab = PairTable(mol)
+    n = mol.nao
+    iu, ju = np.tril_indices(n)
+    p = tab.packidx[iu * n + ju]
+    assert np.array_equal(np.sort(p), np.arange(tab.npack))
+    assert np.array_equal(tab.packidx[ju * n + iu], p)
+    assert np.array_equal(tab.upack[p], tab.sel[iu * n + ju])
+    assert sorted(np.unique(tab.sel)) == sorted(set(range(tab.nsph_tot)))
+    assert sum(len(k) for k in tab.classes.values()) == tab.npair
+    assert tab.nsph_tot == sum(mol.shells[i].nsph * mol.shells[j].nsph for i, j in tab.pairs)
+    # pair of each packed index: both AOs belong to its shells
+    ao_shell = np.repeat(np.arange(len(mol.shells)), [s.nsph for s in mol.shells])
+    for k in (0, tab.npack // 2, tab.npack - 1):
+        mu, nu = iu[np.where(p == k)[0][0]], ju[np.where(p == k)[0][0]]
+        assert tab.pairs[tab.pack_pair[k]] == (ao_shell[mu], ao_shell[nu])
+
+
+def test_f_shell_host_integrals_consistent():
+    """Host McMurchie-Davidson with f shells (the device kernel's reference): the
+    3-index routine with an s aux shell of huge exponent (a point charge) equals the
+    nuclear-attraction routine, and eri_full is 8-fold symmetric."""
+    from xtddft_amd.qc import M
+    shells = [[0, [5.0, 0.6], [0.8, 0.5]], [1, [1.3, 1.0]], [3, [0.9, 1.0]]]
+    mol = M([("O", (0.0, 0.0, 0.0)), ("N", (0.3, -0.2, 1.4))], basis={"O": shells, "N": shells},
+            spin=1, unit="Bohr")
+    eri = mol.eri_full()
+    assert np.abs(eri - eri.transpose(1, 0, 2, 3)).max() < 1e-14
+    assert np.abs(eri - eri.transpose(2, 3, 0, 1)).max() < 1e-13
+    s = 1e24
+    point = {"O": [[0, [s, 1.0]]], "N": [[0, [s, 1.0]]]}
+    aux = M([("O", (0.0, 0.0, 0.0)), ("N", (0.3, -0.2, 1.4))], basis=point, spin=1, unit="Bohr")
+    j3 = mol.int3c2e(aux)                       # aux normalised: (2s/pi)^(3/4) exp(-s r^2)
+    # its charge is (2s/pi)^(3/4) (pi/s)^(3/2): divide it out -> unit point charges
+    q = (s / np.pi) ** 1.5 * (np.pi / (2 * s)) ** 0.75
+    vnuc = -(mol._charges[0] * j3[0] + mol._charges[1] * j3[1]) * q
+    assert np.abs(vnuc - mol.intor("int1e_nuc")).max() < 1e-9 * np.abs(vnuc).max()

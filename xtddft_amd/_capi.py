@@ -29,7 +29,7 @@ EXPORTS = [
     "xt_set_grid", "xt_set_oo_basis", "xt_apply", "xt_dim", "xt_last_timings",
     "xt_xsf_j_diagonals", "xt_set_exchange_mode", "xt_prepare", "xt_set_partition", "xt_set_profile",
     "xt_profile_stats", "xt_profile_bytes", "xt_dgemm", "xt_precond", "xt_row_norms2", "xt_row_scale", "xt_build_id",
-    "xt_int3c2e_cart",
+    "xt_int3c2e_cart", "xt_int2e_cart", "xt_eval_ao",
 ]
 
 
@@ -43,7 +43,7 @@ class XtDesc(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 4   # include/xtddft_amd.h XT_ABI_VERSION
+ABI_VERSION = 5   # include/xtddft_amd.h XT_ABI_VERSION
 
 
 class LibraryMissing(RuntimeError):
@@ -102,6 +102,9 @@ def lib():
     L.xt_row_norms2.argtypes = [c_int, c_int, dp, dp, vp]
     L.xt_row_scale.argtypes = [c_int, c_int, dp, dp, vp]
     L.xt_int3c2e_cart.argtypes = [c_int, vp, dp, dp, c_int, vp, dp, dp, c_int, c_int, c_double, dp, c_long, vp]
+    L.xt_int2e_cart.argtypes = [c_int, vp, dp, dp, c_int, vp, dp, dp, c_int, c_int, c_double, dp, dp, c_double,
+                                c_int, dp, c_long, vp]
+    L.xt_eval_ao.argtypes = [c_int, dp, c_int, vp, dp, dp, dp, c_int, dp, c_long, c_long, vp]
     for name in EXPORTS:
         if not hasattr(L, name):
             raise LibraryMissing(f"{LIB_PATH} lacks symbol {name}")

@@ -1393,11 +1393,31 @@ extern "C" int xt_int3c2e_cart(int npair, const int* pair_info, const double* pa
                                int naux_shells, const int* aux_info, const double* aux_prim, const double* ek,
                                int lmax_orb, int lmax_aux, double omega, double* out, long ldo,
                                void* stream) {
-  if (npair < 0 || naux_shells < 0 || ldo < 0) return fail(XT_ERR_ARG, "xt_int3c2e_cart: negative size");
-  if (lmax_orb > kInt3cMaxLab || lmax_aux > kInt3cMaxLc)
-    return fail(XT_ERR_ARG, "xt_int3c2e_cart: orbital shells up to d and auxiliary shells up to l = 6");
-  if (omega < 0.0) return fail(XT_ERR_ARG, "xt_int3c2e_cart: omega < 0");
-  const int r = int3c2e_cart(npair, pair_info, pair_prim, eab, naux_shells, aux_info, aux_prim, ek, out, ldo,
-                             omega, (hipStream_t)stream);
-  return r ? fail(r, "int3c2e launch failed") : 0;
+  return xt_int2e_cart(npair, pair_info, pair_prim, eab, naux_shells, aux_info, aux_prim, ek, lmax_orb, lmax_aux,
+                       omega, nullptr, nullptr, 0.0, 0, out, ldo, stream);
+}
+
+extern "C" int xt_int2e_cart(int npair, const int* pair_info, const double* pair_prim, const double* eab,
+                             int nket, const int* ket_info, const double* ket_prim, const double* ek,
+                             int lmax_orb, int lket, double omega, const double* q_bra, const double* q_ket,
+                             double q_thr, int diag, double* out, long ldo, void* stream) {
+  if (npair < 0 || nket < 0 || ldo < 0) return fail(XT_ERR_ARG, "xt_int2e_cart: negative size");
+  if (lmax_orb < 0 || lket < 0 || lmax_orb > kIntMaxLOrb || 2 * lmax_orb + lket > kIntMaxL)
+    return fail(XT_ERR_ARG, "xt_int2e_cart: orbital shells up to f and 2 l_orb + l_ket <= 13");
+  if (omega < 0.0) return fail(XT_ERR_ARG, "xt_int2e_cart: omega < 0");
+  if ((q_bra == nullptr) != (q_ket == nullptr)) return fail(XT_ERR_ARG, "xt_int2e_cart: give both bounds or none");
+  if (diag && nket != npair) return fail(XT_ERR_ARG, "xt_int2e_cart: diag needs the ket table = the bra table");
+  const int r = int2e_cart(npair, pair_info, pair_prim, eab, nket, ket_info, ket_prim, ek, lmax_orb, lket, omega,
+                           q_bra, q_ket, q_thr, diag, out, ldo, (hipStream_t)stream);
+  return r ? fail(r, "int2e launch failed") : 0;
+}
+
+extern "C" int xt_eval_ao(int ngrid, const double* coords, int nshell, const int* shell_info,
+                          const double* shell_data, const double* sph, const double* ao_norm, int deriv,
+                          double* out, long ldo, long comp_stride, void* stream) {
+  if (ngrid < 0 || nshell < 0 || ldo < 0 || comp_stride < 0) return fail(XT_ERR_ARG, "xt_eval_ao: negative size");
+  if (deriv != 0 && deriv != 1) return fail(XT_ERR_ARG, "xt_eval_ao: deriv must be 0 or 1");
+  const int r = eval_ao(ngrid, coords, nshell, shell_info, shell_data, sph, ao_norm, deriv, out, ldo, comp_stride,
+                        (hipStream_t)stream);
+  return r ? fail(r, "eval_ao launch failed") : 0;
 }

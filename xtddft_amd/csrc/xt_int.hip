@@ -1,33 +1,41 @@
-// 3-index Coulomb integrals (ab|c) over contracted Cartesian Gaussians on the GPU,
-// by the McMurchie-Davidson scheme: the DF integrals behind the mean field's
-// density-fitting factor (PySCF df.incore.aux_e2 'int3c2e', the factor whose
-// get_jk XTDA.py:518-543 calls and whose MO transform replaces ao2mo.general,
-// XTDA.py:120).  The host restatement is xtddft_amd/qc/ints.py:eri3c.
+// Two-electron Coulomb integrals over contracted Cartesian Gaussians on the GPU, by
+// the McMurchie-Davidson scheme, and the AO values / gradients on the DFT grid --
+// the mean-field front end of SURVEY.md 8(f) row 1:
 //
-//   (ab|c) = sum_{q in pair prims} sum_{r in aux prims} 2 pi^2.5 / (p s sqrt(p + s))
+//  * (ab|c): the DF integrals behind the density-fitting factor (PySCF
+//    df.incore.aux_e2 'int3c2e', the factor whose get_jk XTDA.py:518-543 calls and
+//    whose MO transform replaces ao2mo.general, XTDA.py:120); host restatement
+//    xtddft_amd/qc/ints.py:eri3c;
+//  * (ab|cd): the ket given as shell pairs -- the exact ERIs of the direct-SCF mean
+//    field (PySCF mol.intor('int2e')), as whole blocks, as the diagonal (ab|ab) or as
+//    the pivot columns of the integral-direct Cholesky factorisation (qc/dchol.py);
+//  * point charges as an s "auxiliary" of infinite exponent give the nuclear
+//    attraction (int1e_nuc) through the same kernel;
+//  * ao(g) and grad ao(g) (PySCF eval_ao / ni.block_loop, SF_TDA.py:63-68): one
+//    thread per (grid point, shell).
+//
+//   (ab|c) = sum_{q in pair prims} sum_{r in ket prims} 2 pi^2.5 / (p s sqrt(p + s))
 //            sum_{t in tuv(la+lb)} E^{ab}_t(q) sum_{u in tuv(lc)} (-1)^{|u|} E^c_u(r) R_{t+u}(alpha, P_q - C_r)
 //
 // The Hermite expansion coefficients E (contraction coefficients folded in) are
-// per shell pair / aux shell and cheap: the caller prepares them.  This kernel does
+// per shell pair / ket shell and cheap: the caller prepares them.  The kernel does
 // the quartic part -- Boys functions, the Hermite integrals R_tuv by the downward
-// recursion, and the two contractions -- one thread per (shell pair, aux shell),
-// the R table in private memory.  Not a hot-path kernel (once per mean field).
-// omega > 0 evaluates the long-range operator erf(omega r12)/r12 instead (the
-// range-separated exchange factors; qc/ints.py _attenuate).
+// recursion, and the two contractions -- one thread per (bra pair, ket), the R
+// table in private memory sized by the template bucket (total order L <= 8: d
+// shells; L <= 13: f shells with auxiliary shells up to l = 7 or f f kets).
+// Schwarz screening: with bounds q_bra / q_ket, a (bra, ket) block whose bound
+// product is below q_thr is skipped (left as the caller's zeros).  Not a hot-path
+// kernel (once per mean field).  omega > 0 evaluates the long-range operator
+// erf(omega r12)/r12 instead (the range-separated exchange factors; qc/ints.py
+// _attenuate).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include "xt_internal.h"
 
 namespace xt {
 
-constexpr int I3_MAXLAB = 4;                   // d shells on the orbital side
-constexpr int I3_MAXLC = 6;                    // auxiliary shells up to i (ket pairs up to d d)
-constexpr int I3_MAXL = I3_MAXLAB + I3_MAXLC;
-constexpr int I3_NTUV = (I3_MAXL + 1) * (I3_MAXL + 2) * (I3_MAXL + 3) / 6;
-constexpr int I3_NTAB = (I3_MAXLAB + 1) * (I3_MAXLAB + 2) * (I3_MAXLAB + 3) / 6;
-
-__host__ __device__ inline int ntuv(int L) { return (L + 1) * (L + 2) * (L + 3) / 6; }
-__host__ __device__ inline int ncart(int l) { return (l + 1) * (l + 2) / 2; }
+__host__ __device__ constexpr int ntuv(int L) { return (L + 1) * (L + 2) * (L + 3) / 6; }
+__host__ __device__ constexpr int ncart(int l) { return (l + 1) * (l + 2) / 2; }
 // position of (t, u, v) in the order of qc/ints.py hermite_index: by n = t + u + v,
 // then t descending, then u descending
 __device__ inline int tuv_pos(int t, int u, int v) {
@@ -37,7 +45,7 @@ __device__ inline int tuv_pos(int t, int u, int v) {
 
 // F_n(T), n = 0..m: the series for F_m and downward recursion below T = 30 (all
 // terms positive, no cancellation), F_0 = sqrt(pi/T) erf(sqrt T) / 2 and upward
-// recursion above (e^-T <= 1e-13 against (2n+1) F_n: stable)
+// recursion above (the amplification (2n+1)/(2T) < 1 for n <= 13 < T: stable)
 __device__ void boys_all(int m, double T, double* F) {
   if (T < 30.0) {
     double term = 1.0 / (2 * m + 1), sum = term;
@@ -56,9 +64,11 @@ __device__ void boys_all(int m, double T, double* F) {
   }
 }
 
-// R^0_tuv(alpha, X, Y, Z) for all t + u + v <= L (qc/ints.py hermite_r)
+// R^0_tuv(alpha, X, Y, Z) for all t + u + v <= L (qc/ints.py hermite_r); R and S
+// are two level buffers of ntuv(L) doubles, the result lands in R
+template <int MAXL>
 __device__ void hermite_r(int L, double alpha, double X, double Y, double Z, double* R, double* S) {
-  double F[I3_MAXL + 1];
+  double F[MAXL + 1];
   boys_all(L, alpha * (X * X + Y * Y + Z * Z), F);
   const double m2a = -2.0 * alpha;
   double pw = 1.0;
@@ -92,31 +102,42 @@ __device__ void hermite_r(int L, double alpha, double X, double Y, double Z, dou
 }
 
 // pair_info[8 k + .]: la, lb, npp, prim0, e0, row0;  pair_prim[4 q + .]: p, Px, Py, Pz
-// aux_info[8 j + .]:  lc, nprim, prim0, e0, col0, nc; aux_prim[4 r + .]:  s, Cx, Cy, Cz
+// ket_info[8 j + .]:  lc, nprim, prim0, e0, col0, nc; ket_prim[4 r + .]:  s, Cx, Cy, Cz
 // eab (pair k): [a][b][t][q] over ncart(la) x ncart(lb) x ntuv(la+lb) x npp
-// ek (aux j):   [c][u][r]    over nc x ntuv(lc) x nprim
+// ek (ket j):   [c][u][r]    over nc x ntuv(lc) x nprim
 // The ket may be a shell pair too (4-index (ab|cd)): lc = l_c + l_d, nc = ncart(l_c)
-// ncart(l_d) components, its primitive pairs and Hermite coefficients as the bra's.
+// ncart(l_d), its primitive pairs and Hermite coefficients as the bra's.
+// diag != 0: one thread per bra pair k with the ket j = k (the ERI diagonal blocks).
+template <int MAXL, int MAXLAB>
 __global__ void __launch_bounds__(64)
-k_int3c2e_cart(int npair, const int* __restrict__ pair_info, const double* __restrict__ pair_prim,
-               const double* __restrict__ eab, int naux, const int* __restrict__ aux_info,
-               const double* __restrict__ aux_prim, const double* __restrict__ ek,
-               double* __restrict__ out, long ldo, double omega) {
+k_int_cart(int npair, const int* __restrict__ pair_info, const double* __restrict__ pair_prim,
+           const double* __restrict__ eab, int nket, const int* __restrict__ ket_info,
+           const double* __restrict__ ket_prim, const double* __restrict__ ek, double* __restrict__ out,
+           long ldo, double omega, const double* __restrict__ q_bra, const double* __restrict__ q_ket,
+           double q_thr, int diag) {
   const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= (long)npair * naux) return;
-  const int k = (int)(id / naux), j = (int)(id % naux);
+  int k, j;
+  if (diag) {
+    if (id >= npair) return;
+    k = j = (int)id;
+  } else {
+    if (id >= (long)npair * nket) return;
+    k = (int)(id / nket);
+    j = (int)(id % nket);
+  }
+  if (q_bra != nullptr && q_bra[k] * q_ket[j] < q_thr) return;
   const int* pi = pair_info + 8 * k;
-  const int* ai = aux_info + 8 * j;
+  const int* ai = ket_info + 8 * j;
   const int la = pi[0], lb = pi[1], npp = pi[2], pq0 = pi[3], pe0 = pi[4], row0 = pi[5];
   const int lc = ai[0], nr = ai[1], ar0 = ai[2], ae0 = ai[3], col0 = ai[4];
   const int lab = la + lb, L = lab + lc;
   const int nab = ncart(la) * ncart(lb), ntab = ntuv(lab), nc = ai[5], ntc = ntuv(lc);
-  double R[I3_NTUV], S[I3_NTUV], M[I3_NTAB];
+  double R[ntuv(MAXL)], S[ntuv(MAXL)], M[ntuv(MAXLAB)];
   for (int q = 0; q < npp; ++q) {
     const double* pp = pair_prim + 4 * (long)(pq0 + q);
     const double p = pp[0];
     for (int r = 0; r < nr; ++r) {
-      const double* cp = aux_prim + 4 * (long)(ar0 + r);
+      const double* cp = ket_prim + 4 * (long)(ar0 + r);
       const double s = cp[0];
       double alpha = p * s / (p + s), scale = 1.0;
       if (omega > 0.0) {   // erf(omega r)/r: 1/a' = 1/alpha + 1/omega^2, times sqrt(a'/alpha)
@@ -124,7 +145,7 @@ k_int3c2e_cart(int npair, const int* __restrict__ pair_info, const double* __res
         scale = sqrt(a2 / alpha);
         alpha = a2;
       }
-      hermite_r(L, alpha, pp[1] - cp[1], pp[2] - cp[2], pp[3] - cp[3], R, S);
+      hermite_r<MAXL>(L, alpha, pp[1] - cp[1], pp[2] - cp[2], pp[3] - cp[3], R, S);
       const double pref = 2.0 * pow(M_PI, 2.5) / (p * s * sqrt(p + s)) * scale;
       for (int c = 0; c < nc; ++c) {
         // M[t] = sum_u (-1)^{|u|} E^c_u(r) R[t + u]
@@ -154,14 +175,108 @@ k_int3c2e_cart(int npair, const int* __restrict__ pair_info, const double* __res
   }
 }
 
-int int3c2e_cart(int npair, const int* pair_info, const double* pair_prim, const double* eab, int naux_shells,
-                 const int* aux_info, const double* aux_prim, const double* ek, double* out, long ldo,
-                 double omega, hipStream_t st) {
-  const long n = (long)npair * naux_shells;
+int int2e_cart(int npair, const int* pair_info, const double* pair_prim, const double* eab, int nket,
+               const int* ket_info, const double* ket_prim, const double* ek, int lmax_orb, int lket,
+               double omega, const double* q_bra, const double* q_ket, double q_thr, int diag, double* out,
+               long ldo, hipStream_t st) {
+  const long n = diag ? (long)npair : (long)npair * nket;
   if (n == 0) return 0;
   const int blk = 64;
-  hipLaunchKernelGGL(k_int3c2e_cart, dim3((unsigned)((n + blk - 1) / blk)), dim3(blk), 0, st, npair, pair_info,
-                     pair_prim, eab, naux_shells, aux_info, aux_prim, ek, out, ldo, omega);
+  const dim3 grid((unsigned)((n + blk - 1) / blk));
+  if (2 * lmax_orb <= 4 && 2 * lmax_orb + lket <= 8)
+    hipLaunchKernelGGL((k_int_cart<8, 4>), grid, dim3(blk), 0, st, npair, pair_info, pair_prim, eab, nket,
+                       ket_info, ket_prim, ek, out, ldo, omega, q_bra, q_ket, q_thr, diag);
+  else if (2 * lmax_orb <= 6 && 2 * lmax_orb + lket <= kIntMaxL)
+    hipLaunchKernelGGL((k_int_cart<kIntMaxL, 6>), grid, dim3(blk), 0, st, npair, pair_info, pair_prim, eab,
+                       nket, ket_info, ket_prim, ek, out, ldo, omega, q_bra, q_ket, q_thr, diag);
+  else
+    return XT_ERR_ARG;
+  return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
+}
+
+// ---------------------------------------------------------------- AO on the grid
+// shell_info[8 s + .]: l, nprim, data offset (exponents, then coefficients x radial
+// norms, then the centre), first AO; sph: real solid-harmonic tables of l = 0..4
+// (libcint order, qc/gto.py _sph_transform) concatenated; norm: per-AO normalisation.
+// out[c * comp_stride + g * ldo + ao] for c = value (, d/dx, d/dy, d/dz).
+__global__ void __launch_bounds__(256)
+k_eval_ao(int ngrid, const double* __restrict__ coords, int nshell, const int* __restrict__ shell_info,
+          const double* __restrict__ dat, const double* __restrict__ sph, const double* __restrict__ norm,
+          int deriv, double* __restrict__ out, long ldo, long comp_stride) {
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long)ngrid * nshell) return;
+  const int g = (int)(id / nshell), s = (int)(id % nshell);
+  const int* si = shell_info + 8 * s;
+  const int l = si[0], np = si[1], off = si[2], ao0 = si[3];
+  const double* ex = dat + off;
+  const double* cf = ex + np;
+  const double* ctr = cf + np;
+  const double dx = coords[3 * (long)g] - ctr[0], dy = coords[3 * (long)g + 1] - ctr[1],
+               dz = coords[3 * (long)g + 2] - ctr[2];
+  const double r2 = dx * dx + dy * dy + dz * dz;
+  double g0 = 0.0, g1 = 0.0;
+  for (int k = 0; k < np; ++k) {
+    const double e = cf[k] * exp(-ex[k] * r2);
+    g0 += e;
+    g1 -= 2.0 * ex[k] * e;
+  }
+  // powers d^0..d^l per direction
+  double px[kAoMaxL + 1], py[kAoMaxL + 1], pz[kAoMaxL + 1];
+  px[0] = py[0] = pz[0] = 1.0;
+  for (int i = 1; i <= l; ++i) {
+    px[i] = px[i - 1] * dx;
+    py[i] = py[i - 1] * dy;
+    pz[i] = pz[i - 1] * dz;
+  }
+  constexpr int NC = ncart(kAoMaxL);
+  double cv[NC], cgx[NC], cgy[NC], cgz[NC];
+  int c = 0;
+  for (int ix = l; ix >= 0; --ix)
+    for (int iy = l - ix; iy >= 0; --iy, ++c) {
+      const int iz = l - ix - iy;
+      const double poly = px[ix] * py[iy] * pz[iz];
+      cv[c] = poly * g0;
+      if (deriv) {
+        const double pg = poly * g1;
+        cgx[c] = (ix ? ix * px[ix - 1] * py[iy] * pz[iz] * g0 : 0.0) + pg * dx;
+        cgy[c] = (iy ? iy * px[ix] * py[iy - 1] * pz[iz] * g0 : 0.0) + pg * dy;
+        cgz[c] = (iz ? iz * px[ix] * py[iy] * pz[iz - 1] * g0 : 0.0) + pg * dz;
+      }
+    }
+  const int nc = ncart(l), ns = 2 * l + 1;
+  int toff = 0;
+  for (int k = 0; k < l; ++k) toff += (2 * k + 1) * ncart(k);
+  const double* T = sph + toff;
+  double* o = out + (long)g * ldo + ao0;
+  for (int m = 0; m < ns; ++m) {
+    double v = 0.0, vx = 0.0, vy = 0.0, vz = 0.0;
+    for (int k = 0; k < nc; ++k) {
+      const double t = T[m * nc + k];
+      v += t * cv[k];
+      if (deriv) {
+        vx += t * cgx[k];
+        vy += t * cgy[k];
+        vz += t * cgz[k];
+      }
+    }
+    const double nm = norm[ao0 + m];
+    o[m] = nm * v;
+    if (deriv) {
+      o[comp_stride + m] = nm * vx;
+      o[2 * comp_stride + m] = nm * vy;
+      o[3 * comp_stride + m] = nm * vz;
+    }
+  }
+}
+
+int eval_ao(int ngrid, const double* coords, int nshell, const int* shell_info, const double* dat,
+            const double* sph, const double* norm, int deriv, double* out, long ldo, long comp_stride,
+            hipStream_t st) {
+  const long n = (long)ngrid * nshell;
+  if (n == 0) return 0;
+  const int blk = 256;
+  hipLaunchKernelGGL(k_eval_ao, dim3((unsigned)((n + blk - 1) / blk)), dim3(blk), 0, st, ngrid, coords, nshell,
+                     shell_info, dat, sph, norm, deriv, out, ldo, comp_stride);
   return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
 }
 

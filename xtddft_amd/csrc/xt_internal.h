@@ -88,11 +88,16 @@ int xc_back_m(int O, int nx, int V, int n, const double* PO, long ldp, const dou
 // PhiO[g][i] Zp[i zi + xg zx + a]; reads Zp up to 7 rows past O and WA - 1 columns past
 // V (zeroed slack), grid arrays XC_GRID_SLACK rows past n
 size_t xc_rho_w_lds_bytes(int O);
-// 3-index Coulomb integrals over Cartesian Gaussians (xt_int.hip); orbital l <= 2, aux l <= 6
-constexpr int kInt3cMaxLab = 2, kInt3cMaxLc = 6;
-int int3c2e_cart(int npair, const int* pair_info, const double* pair_prim, const double* eab, int naux_shells,
-                 const int* aux_info, const double* aux_prim, const double* ek, double* out, long ldo,
-                 double omega, hipStream_t st);
+// Coulomb integrals over Cartesian Gaussians and AO values on the grid (xt_int.hip):
+// orbital l <= 3, total Hermite order 2 l_orb + l_ket <= kIntMaxL; AO values l <= kAoMaxL
+constexpr int kIntMaxLOrb = 3, kIntMaxL = 13, kAoMaxL = 4;
+int int2e_cart(int npair, const int* pair_info, const double* pair_prim, const double* eab, int nket,
+               const int* ket_info, const double* ket_prim, const double* ek, int lmax_orb, int lket,
+               double omega, const double* q_bra, const double* q_ket, double q_thr, int diag, double* out,
+               long ldo, hipStream_t st);
+int eval_ao(int ngrid, const double* coords, int nshell, const int* shell_info, const double* dat,
+            const double* sph, const double* norm, int deriv, double* out, long ldo, long comp_stride,
+            hipStream_t st);
 int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const double* Z, long zi, long zx,
              const double* W, long wc, long wg, double* R, long rg, hipStream_t st);
 size_t dgemm_workspace_bytes(const GemmDesc& d);

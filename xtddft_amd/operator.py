@@ -192,9 +192,14 @@ class DeviceOperator:
             grids = mf.grids
             sf = self.kind in ("SF_DOWN", "SF_UP", "XSF")
             ao = grids.ao[:1, g0:g1] if sf else grids.ao[:, g0:g1]
-            pao, kao, rao = _ptr(ao)
-            pw, kw, rw = _ptr(grids.weights[g0:g1])
+            w = grids.weights[g0:g1]
             kern = mf.fxc_sf[g0:g1] if sf else mf.fxc[..., g0:g1]
+            if _is_device(ao):       # AO values resident in HBM (device eval_ao): kernel data follows
+                torch = _torch()
+                w, kern = (x if _is_device(x) else torch.as_tensor(np.ascontiguousarray(x), device=ao.device)
+                           for x in (w, kern))
+            pao, kao, rao = _ptr(ao)
+            pw, kw, rw = _ptr(w)
             pk, kk, rk = _ptr(kern)
             if not (kao == kw == kk):
                 raise TypeError("grid arrays must all be host or all device")

@@ -4,8 +4,14 @@ DF factor and the grid resident in HBM ("ROKS/UKS SCF
 driver reusing the HIP J/K + XC kernels").
 
 * J[D] = sum_P B_P <B_P, D>: two GEMMs over the pair index;
-* K[D] = sum_P B_P D B_P: T = B^(mP) D then K = T B over (P, l) -- two GEMMs on
-  the factor kept in both (P, m, l) and (m, P, l) layouts;
+* K[D] = sum_P B_P D B_P for a symmetric D = V diag(lam) V^T (host eigh of the
+  small density, |lam| > 1e-14 kept -- the occupied factorisation gpu4pyscf's
+  tagged densities give, XTDA_GPU.py:232): T = B V (one GEMM), then
+  K = T' diag(lam) T'^T over (P, i) (one GEMM), 2 naux nao^2 rank x 2 flop instead
+  of 4 naux nao^3; a non-symmetric D takes the plain B D B route;
+* the factor is the DF factor, the device integral-direct Cholesky factor of the
+  exact ERIs (``qc.dchol``, already in HBM), or the pivoted Cholesky of stored
+  ERIs (small molecules);
 * rho, grad rho from C = Phi_0 D (GEMM) and row dots; V_xc = Phi_0^T (sum_y wv_y
   Phi_y) (+ transpose for GGA) as GEMMs; the functional and its first / second
   derivatives (vxc, the cached fxc of ``cache_xc_kernel``, XTDA.py:504, and the
@@ -37,14 +43,18 @@ class DeviceEngine:
         self.n = n
         if mf.with_df is not None:
             b = np.asarray(mf.with_df.cderi)
-        else:   # exact ERIs: their pivoted Cholesky factor is an exact "DF" factor
+        elif getattr(mf, "cderi_exact", None) is not None:
+            b = mf.cderi_exact                 # device tensor from qc.dchol
+        else:   # stored exact ERIs: their pivoted Cholesky factor is an exact "DF" factor
             from .scf import pivoted_cholesky
             b = pivoted_cholesky(mf.eri.reshape(n * n, n * n), 1e-14).reshape(-1, n, n)
         self.naux = b.shape[0]
-        self.B = torch.as_tensor(np.ascontiguousarray(b), device=self.dev)              # (P, m, l)
-        self.Bt = self.B.permute(1, 0, 2).contiguous()                                  # (m, P, l)
+        self.B = b.to(self.dev).contiguous() if isinstance(b, torch.Tensor) else \
+            torch.as_tensor(np.ascontiguousarray(b), device=self.dev)                    # (P, m, l)
         if mf.xctype != "HF":
-            self.ao = torch.as_tensor(np.ascontiguousarray(mf.ao), device=self.dev)      # (ncomp, G, n)
+            ao = mf.ao
+            self.ao = ao.to(self.dev) if isinstance(ao, torch.Tensor) else \
+                torch.as_tensor(np.ascontiguousarray(ao), device=self.dev)               # (ncomp, G, n)
             self.w = torch.as_tensor(np.ascontiguousarray(mf.grids.weights), device=self.dev)
 
     # ------------------------------------------------------------ GEMM
@@ -76,12 +86,25 @@ class DeviceEngine:
             gam = self._mm(b2, dt.reshape(-1, n * n), tb=1)                  # (P, nset)
             vj = self._mm(gam, b2, ta=1).reshape(shape).cpu().numpy()        # (nset, n^2)
         if with_k:
-            out = []
-            for x in range(dt.shape[0]):
-                t = self._mm(self.Bt.reshape(n * P, n), dt[x])               # [(m, P), l] = (B_P D)[m, l]
-                out.append(self._mm(t.reshape(n, P * n), self.B.reshape(P * n, n)))
-            vk = torch.stack(out).reshape(shape).cpu().numpy()
+            vk = np.stack([self._k(d.reshape(-1, n, n)[x], dt[x]) for x in range(dt.shape[0])]).reshape(shape)
         return vj, vk
+
+    def _k(self, dh, dd):
+        """K[D] (host array) for one density (dh host, dd the same on the device)."""
+        torch = self.torch
+        n, P = self.n, self.naux
+        if np.abs(dh - dh.T).max() <= 1e-14 * max(1.0, np.abs(dh).max()):
+            lam, v = np.linalg.eigh(0.5 * (dh + dh.T))
+            keep = np.abs(lam) > 1e-14 * max(1.0, np.abs(lam).max())
+            r = int(keep.sum())
+            if r == 0:
+                return np.zeros((n, n))
+            vt = torch.as_tensor(np.ascontiguousarray(v[:, keep]), device=self.dev)
+            t = self._mm(self.B.reshape(P * n, n), vt).reshape(P, n, r).permute(1, 0, 2).contiguous()
+            ts = t * torch.as_tensor(lam[keep], device=self.dev)
+            return self._mm(t.reshape(n, P * r), ts.reshape(n, P * r), tb=1).cpu().numpy()
+        t = self._mm(self.B.reshape(P * n, n), dd).reshape(P, n, n).permute(1, 0, 2).contiguous()
+        return self._mm(t.reshape(n, P * n), self.B.reshape(P * n, n)).cpu().numpy()
 
     # ------------------------------------------------------------ XC
     def _rho(self, dm):

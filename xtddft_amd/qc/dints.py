@@ -1,21 +1,31 @@
-"""Two-electron integrals on the GPU (the device integral path):
-the 3-index DF integrals and the 4-index ERIs of the exact-exchange path.
+"""Integrals on the GPU (the device integral path).
 
-``int3c2e_device(mol, auxmol)`` returns the same (naux, nao, nao) tensor as
-``Mole.int3c2e`` (PySCF ``df.incore.aux_e2(mol, auxmol, 'int3c2e')``, aux-major):
+Everything here goes through two library kernels (``csrc/xt_int.hip``):
 
-* per shell pair (i >= j) and per auxiliary shell the host prepares the Hermite
-  expansion coefficients (``ints.ShellPair.Eab``, ``ints.AuxShellSet.Ek``: O(primitives)
-  work);
-* ``xt_int3c2e_cart`` (``csrc/xt_int.hip``) evaluates the quartic part on the
-  device -- Boys functions, Hermite integrals, both contractions -- into one
-  Cartesian matrix (pair components x auxiliary components);
-* the spherical transforms are two ``xt_dgemm`` products with block-diagonal
-  Cartesian -> solid-harmonic matrices; the (mu nu) <-> (nu mu) fill is one gather
-  of pair rows and the AO / auxiliary normalisation element-wise, on the device.
+* ``xt_int2e_cart`` -- McMurchie-Davidson Coulomb integrals between shell pairs
+  (the bra) and a ket table (auxiliary shells, shell pairs, or point charges),
+  orbital shells up to f;
+* ``xt_eval_ao`` -- AO values and gradients on grid points.
 
-``eri_full_device(mol)`` returns ``Mole.eri_full`` (PySCF ``mol.intor('int2e')``)
-the same way, the ket given to the kernel as the same shell pairs.
+The host prepares only per-shell-pair data (``ints.ShellPair.Eab``: Hermite
+coefficients, O(primitives) work) once per molecule (``PairTable``, cached on the
+``Mole``).  The Cartesian -> spherical transform is block-sparse: pairs are grouped
+by (l_i, l_j) class and each class is one batched product with kron(T_li, T_lj) --
+no dense transform matrix exists, so the memory stays O(pairs) at any size.
+
+Entry points (all return what the host routines of ``gto.Mole`` return; tests
+compare them to 1e-12):
+
+* ``int3c2e_device``   -- (P|mu nu), PySCF ``df.incore.aux_e2`` (aux-major);
+* ``eri_full_device``  -- (mu nu|la si), PySCF ``mol.intor('int2e')`` (small molecules);
+* ``eri_diag_device`` / ``eri_columns_device`` -- the diagonal (mu nu|mu nu) and the
+  columns (all pairs | chosen shell pairs) in the packed pair index
+  mu (mu+1)/2 + nu, mu >= nu: the two integral requests of the integral-direct
+  Cholesky factorisation (``qc/dchol.py``);
+* ``int1e_nuc_device`` -- sum_C -Z_C <mu|1/|r-C||nu> (point charges as s shells of
+  exponent 1e24 with coefficient (s/pi)^1.5: the kernel's prefactor then tends to
+  PySCF's 2 pi / p to 1e-20 relative);
+* ``eval_ao_device``   -- AO values (+ gradients) on grid points (PySCF ``eval_ao``).
 """
 from __future__ import annotations
 
@@ -27,31 +37,167 @@ from .. import _capi
 from .gto import _sph_transform
 from .ints import AuxShellSet, ShellPair
 
-
-def _block_transform(shells):
-    """Block-diagonal (n_sph_total, n_cart_total) Cartesian -> spherical matrix."""
-    ns = sum(s.nsph for s in shells)
-    nc = sum(s.ncart for s in shells)
-    T = np.zeros((ns, nc))
-    r = c = 0
-    for s in shells:
-        T[r:r + s.nsph, c:c + s.ncart] = _sph_transform(s.l)
-        r += s.nsph
-        c += s.ncart
-    return T
+POINT_CHARGE_EXP = 1e24
+AO_MAX_L = 4
 
 
-def int3c2e_device(mol, auxmol, device: int = 0, omega: float = 0.0):
+def _torch():
+    import torch
+    return torch
+
+
+class PairTable:
+    """Shell pairs i >= j of a Mole: the kernel tables, the block-sparse spherical
+    transform and the index maps (spherical pair rows, packed pair index)."""
+
+    def __init__(self, mol):
+        sh = mol.shells
+        n = mol.nao
+        self.nao = n
+        pinfo, pprim, eab, pairs = [], [], [], []
+        c0s, s0s = [], []
+        crow = srow = q0 = e0 = 0
+        for i in range(len(sh)):
+            for j in range(i + 1):
+                sp = ShellPair(sh[i], sh[j])
+                nca, ncb, _, npp = sp.Eab.shape
+                pinfo.append([sh[i].l, sh[j].l, npp, q0, e0, crow, 0, 0])
+                pprim.append(np.column_stack([sp.p, sp.P]))
+                eab.append(sp.Eab.ravel())
+                pairs.append((i, j))
+                c0s.append(crow)
+                s0s.append(srow)
+                crow += nca * ncb
+                srow += sh[i].nsph * sh[j].nsph
+                q0 += npp
+                e0 += sp.Eab.size
+        self.pinfo = np.array(pinfo, dtype=np.int32)
+        self.pprim = np.concatenate(pprim)
+        self.eab = np.concatenate(eab)
+        self.pairs = pairs
+        self.npair = len(pairs)
+        self.c0 = np.array(c0s, dtype=np.int64)
+        self.s0 = np.array(s0s, dtype=np.int64)
+        self.ncart_tot, self.nsph_tot = crow, srow
+        self.lmax = max(s.l for s in sh)
+        # spherical row of every (mu, nu) (either order), row norms, pair of each row
+        sel = np.empty(n * n, dtype=np.int64)
+        wrow = np.empty(srow)
+        self.nab = np.empty(self.npair, dtype=np.int64)
+        self.nsab = np.empty(self.npair, dtype=np.int64)
+        nrm = mol._norm
+        classes = {}
+        for k, (i, j) in enumerate(pairs):
+            si, sj = sh[i], sh[j]
+            mu = mol.ao_loc[i] + np.arange(si.nsph)[:, None]
+            nu = mol.ao_loc[j] + np.arange(sj.nsph)[None, :]
+            rows = s0s[k] + np.arange(si.nsph * sj.nsph).reshape(si.nsph, sj.nsph)
+            sel[(mu * n + nu).ravel()] = rows.ravel()
+            sel[(nu * n + mu).ravel()] = rows.ravel()
+            wrow[rows.ravel()] = (nrm[mu] * nrm[nu]).ravel()
+            self.nab[k] = si.ncart * sj.ncart
+            self.nsab[k] = si.nsph * sj.nsph
+            classes.setdefault((si.l, sj.l), []).append(k)
+        self.sel = sel
+        self.wrow = wrow
+        self.classes = {key: np.array(v, dtype=np.int64) for key, v in classes.items()}
+        # packed pair index p = mu (mu + 1) / 2 + nu (mu >= nu) -> spherical row, pair id
+        iu, ju = np.tril_indices(n)
+        self.npack = iu.size
+        packidx = np.empty(n * n, dtype=np.int64)
+        pidx = iu * (iu + 1) // 2 + ju
+        packidx[iu * n + ju] = pidx
+        packidx[ju * n + iu] = pidx
+        order = np.argsort(pidx)
+        self.upack = sel[(iu * n + ju)[order]]                 # spherical row of packed index p
+        self.packidx = packidx                                 # (mu, nu) -> packed index
+        row_pair = np.empty(srow, dtype=np.int64)
+        for k in range(self.npair):
+            row_pair[s0s[k]:s0s[k] + self.nsab[k]] = k
+        self.pack_pair = row_pair[self.upack]                  # shell pair of packed index p
+        self._dev = {}
+
+    # ------------------------------------------------------------ device copies
+    def dev(self, device):
+        """Kernel tables and transform blocks on GPU ``device`` (cached)."""
+        if device in self._dev:
+            return self._dev[device]
+        torch = _torch()
+        dv = torch.device(f"cuda:{device}")
+
+        def t(x, dtype=torch.float64):
+            return torch.as_tensor(np.ascontiguousarray(x), dtype=dtype, device=dv)
+        d = dict(dev=dv, pinfo=t(self.pinfo, torch.int32), pprim=t(self.pprim), eab=t(self.eab),
+                 wrow=t(self.wrow), upack=t(self.upack, torch.int64), sel=t(self.sel, torch.int64),
+                 packidx=t(self.packidx, torch.int64), pack_pair=t(self.pack_pair, torch.int64))
+        cls = []
+        for (li, lj), ks in self.classes.items():
+            Tk = np.kron(_sph_transform(li), _sph_transform(lj))
+            ns, nc = Tk.shape
+            cidx = self.c0[ks][:, None] + np.arange(nc)[None, :]
+            sidx = self.s0[ks][:, None] + np.arange(ns)[None, :]
+            cls.append((t(Tk), t(cidx, torch.int64), t(sidx, torch.int64), ks))
+        d["classes"] = cls
+        self._dev[device] = d
+        return d
+
+    # ------------------------------------------------------------ transforms
+    def rows_to_sph(self, x, device):
+        """(ncart_tot, m) Cartesian pair rows -> (nsph_tot, m) normalised spherical rows."""
+        torch = _torch()
+        d = self.dev(device)
+        y = torch.empty((self.nsph_tot, x.shape[1]), dtype=torch.float64, device=d["dev"])
+        for Tk, cidx, sidx, _ in d["classes"]:
+            y[sidx.reshape(-1)] = torch.matmul(Tk, x[cidx]).reshape(-1, x.shape[1])
+        y *= d["wrow"][:, None]
+        return y
+
+    def ket_info_pairs(self, ks, col_offsets=None):
+        """Ket table (8 ints per entry) giving shell pairs ``ks`` as kets, output
+        columns from ``col_offsets`` (default: consecutive Cartesian blocks)."""
+        p = self.pinfo[ks]
+        out = np.zeros((len(ks), 8), dtype=np.int32)
+        out[:, 0] = p[:, 0] + p[:, 1]
+        out[:, 1:4] = p[:, 2:5]
+        nab = self.nab[ks]
+        out[:, 4] = np.concatenate([[0], np.cumsum(nab)[:-1]]) if col_offsets is None else col_offsets
+        out[:, 5] = nab
+        return out
+
+
+def pair_table(mol) -> PairTable:
+    tab = getattr(mol, "_pair_table", None)
+    if tab is None:
+        tab = PairTable(mol)
+        mol._pair_table = tab
+    return tab
+
+
+def _stream(device):
+    torch = _torch()
+    return ctypes.c_void_p(torch.cuda.current_stream(torch.device(f"cuda:{device}")).cuda_stream)
+
+
+def _launch(L, tab, d, nket, kinfo, kprim, ek, lket, omega, out, ldo, device, qb=None, qk=None, thr=0.0,
+            diag=0):
+    _capi.check(L.xt_int2e_cart(tab.npair, d["pinfo"].data_ptr(), d["pprim"].data_ptr(), d["eab"].data_ptr(),
+                                nket, kinfo.data_ptr(), kprim.data_ptr(), ek.data_ptr(), tab.lmax, int(lket),
+                                float(omega), None if qb is None else qb.data_ptr(),
+                                None if qk is None else qk.data_ptr(), float(thr), int(diag), out.data_ptr(),
+                                int(ldo), _stream(device)), "xt_int2e_cart")
+
+
+# ---------------------------------------------------------------- 3-index DF
+def int3c2e_device(mol, auxmol, device: int = 0, omega: float = 0.0, as_tensor: bool = False):
     """(P|mu nu) over normalised spherical functions, (naux, nao, nao), on the GPU
     (omega > 0: erf(omega r12)/r12)."""
-    import torch
+    torch = _torch()
     L = _capi.lib()
-    dev = torch.device(f"cuda:{device}")
-    sh, ash = mol.shells, auxmol.shells
+    tab = pair_table(mol)
+    d = tab.dev(device)
+    dv = d["dev"]
+    ash = auxmol.shells
     n, naux = mol.nao, auxmol.nao
-    pinfo, pprim, eab, prow, nrow = _pairs(mol)
-    tp, sel = _pair_sph(mol, prow, nrow)
-    # auxiliary shells
     ainfo, aprim, ek = [], [], []
     col = r0 = e0 = 0
     for s in ash:
@@ -64,118 +210,194 @@ def int3c2e_device(mol, auxmol, device: int = 0, omega: float = 0.0):
         e0 += a.Ek.size
     ncol = col
 
-    def dt(x, dtype=torch.float64):
-        return torch.as_tensor(np.ascontiguousarray(x), dtype=dtype, device=dev)
-    t_pinfo, t_pprim, t_eab = dt(pinfo, torch.int32), dt(pprim), dt(eab)
-    t_ainfo = dt(np.array(ainfo, dtype=np.int32), torch.int32)
-    t_aprim, t_ek = dt(np.concatenate(aprim)), dt(np.concatenate(ek))
-    cart = torch.zeros((nrow, ncol), dtype=torch.float64, device=dev)
-    with torch.cuda.device(dev):
-        st = torch.cuda.current_stream(dev).cuda_stream
-        _capi.check(L.xt_int3c2e_cart(len(prow), t_pinfo.data_ptr(), t_pprim.data_ptr(), t_eab.data_ptr(),
-                                      len(ash), t_ainfo.data_ptr(), t_aprim.data_ptr(), t_ek.data_ptr(),
-                                      max(s.l for s in sh), max(s.l for s in ash), float(omega), cart.data_ptr(),
-                                      ncol, ctypes.c_void_p(st)), "xt_int3c2e_cart")
-        # spherical on both sides (pair blocks Ti (x) Tj, aux blocks Ta), then the
-        # (mu nu) fill as one gather of pair rows
-        ysph = _mm(L, st, dev, _mm(L, st, dev, dt(tp), cart), dt(_block_transform(ash)), tb=1)   # (npair_sph, naux)
-        out = ysph.index_select(0, dt(sel, torch.int64)).t().reshape(naux, n, n)
-        nrm = dt(mol._norm)
-        out *= dt(auxmol._norm)[:, None, None] * nrm[None, :, None] * nrm[None, None, :]
-        return out.cpu().numpy()
+    def t(x, dtype=torch.float64):
+        return torch.as_tensor(np.ascontiguousarray(x), dtype=dtype, device=dv)
+    with torch.cuda.device(dv):
+        cart = torch.zeros((tab.ncart_tot, ncol), dtype=torch.float64, device=dv)
+        _launch(L, tab, d, len(ash), t(np.array(ainfo, dtype=np.int32), torch.int32), t(np.concatenate(aprim)),
+                t(np.concatenate(ek)), max(s.l for s in ash), omega, cart, ncol, device)
+        y = tab.rows_to_sph(cart, device)                                   # (nsph_tot, ncart_aux)
+        del cart
+        ta = torch.block_diag(*[t(_sph_transform(s.l)) for s in ash])       # (naux, ncart_aux)
+        ysph = torch.matmul(y, ta.T)                                        # (nsph_tot, naux)
+        out = ysph.index_select(0, d["sel"]).T.reshape(naux, n, n)
+        out = out * t(auxmol._norm)[:, None, None]
+        return out if as_tensor else out.cpu().numpy()
 
 
-def _mm(L, st, dev, a, b, ta=0, tb=0):
-    """op(a) @ op(b) for 2-D contiguous device tensors through the library's FP64 MFMA GEMM."""
-    import torch
-    m = a.shape[1] if ta else a.shape[0]
-    k = a.shape[0] if ta else a.shape[1]
-    nn = b.shape[0] if tb else b.shape[1]
-    c = torch.empty((m, nn), dtype=torch.float64, device=dev)
-    _capi.check(L.xt_dgemm(ta, tb, m, nn, k, 1.0, a.data_ptr(), a.shape[1], b.data_ptr(), b.shape[1],
-                           0.0, c.data_ptr(), nn, ctypes.c_void_p(st)), "xt_dgemm")
-    return c
-
-
-def _pair_sph(mol, prow, ncart_tot):
-    """Block-diagonal pair Cartesian -> spherical matrix (Ti (x) Tj per pair) and, per
-    full index mu * n + nu, the spherical pair row that holds it (either order)."""
-    sh, n = mol.shells, mol.nao
-    nsph_tot = sum(sh[i].nsph * sh[j].nsph for i, j, _ in prow)
-    tp = np.zeros((nsph_tot, ncart_tot))
-    sel = np.empty(n * n, dtype=np.int64)
-    r = 0
-    for i, j, c0 in prow:
-        si, sj = sh[i], sh[j]
-        tp[r:r + si.nsph * sj.nsph, c0:c0 + si.ncart * sj.ncart] = np.kron(_sph_transform(si.l),
-                                                                          _sph_transform(sj.l))
-        mu = mol.ao_loc[i] + np.arange(si.nsph)[:, None]
-        nu = mol.ao_loc[j] + np.arange(sj.nsph)[None, :]
-        rows = r + np.arange(si.nsph * sj.nsph).reshape(si.nsph, sj.nsph)
-        sel[(mu * n + nu).ravel()] = rows.ravel()
-        sel[(nu * n + mu).ravel()] = rows.ravel()
-        r += si.nsph * sj.nsph
-    return tp, sel
-
-
-def _pairs(mol):
-    """Shell pairs i >= j: kernel tables (pair_info, pair_prim, eab) and per pair
-    (i, j, first Cartesian row)."""
-    sh = mol.shells
-    pinfo, pprim, eab, prow = [], [], [], []
-    row = q0 = e0 = 0
-    for i in range(len(sh)):
-        for j in range(i + 1):
-            sp = ShellPair(sh[i], sh[j])
-            nca, ncb, _, npp = sp.Eab.shape
-            pinfo.append([sh[i].l, sh[j].l, npp, q0, e0, row, 0, 0])
-            pprim.append(np.column_stack([sp.p, sp.P]))
-            eab.append(sp.Eab.ravel())
-            prow.append((i, j, row))
-            row += nca * ncb
-            q0 += npp
-            e0 += sp.Eab.size
-    return np.array(pinfo, dtype=np.int32), np.concatenate(pprim), np.concatenate(eab), prow, row
-
-
+# ---------------------------------------------------------------- 4-index
 def eri_full_device(mol, device: int = 0, omega: float = 0.0):
     """(mu nu|la si) over normalised spherical AOs, all 8 symmetry copies (as
-    ``Mole.eri_full``, PySCF ``mol.intor('int2e')``), on the GPU: the bra and the
-    ket are the same shell-pair tables, the Cartesian (pair x pair) matrix comes
-    from ``xt_int3c2e_cart`` with the ket given as pairs, the spherical transform
-    is two ``xt_dgemm`` products and the symmetric fill one gather."""
-    import torch
+    ``Mole.eri_full``, PySCF ``mol.intor('int2e')``), on the GPU: bra and ket are
+    the same shell-pair table; exact (ab|cd) = (cd|ab) by symmetrising."""
+    torch = _torch()
     L = _capi.lib()
-    dev = torch.device(f"cuda:{device}")
-    sh = mol.shells
+    tab = pair_table(mol)
+    d = tab.dev(device)
+    dv = d["dev"]
     n = mol.nao
-    pinfo, pprim, eab, prow, ncart_tot = _pairs(mol)
-    ainfo = np.zeros_like(pinfo)                 # the ket: the same pairs
-    ainfo[:, 0] = pinfo[:, 0] + pinfo[:, 1]
-    ainfo[:, 1:5] = pinfo[:, 2:6]
-    ainfo[:, 5] = [sh[i].ncart * sh[j].ncart for i, j, _ in prow]
+    kinfo = torch.as_tensor(tab.ket_info_pairs(np.arange(tab.npair), tab.c0.astype(np.int32)), device=dv)
+    with torch.cuda.device(dv):
+        cart = torch.zeros((tab.ncart_tot, tab.ncart_tot), dtype=torch.float64, device=dv)
+        _launch(L, tab, d, tab.npair, kinfo, d["pprim"], d["eab"], 2 * tab.lmax, omega, cart, tab.ncart_tot, device)
+        y = tab.rows_to_sph(tab.rows_to_sph(cart, device).T.contiguous(), device)   # (nsph, nsph), symmetric
+        y = 0.5 * (y + y.T)
+        return y.index_select(0, d["sel"]).index_select(1, d["sel"]).reshape(n, n, n, n).cpu().numpy()
 
-    def dt(x, dtype=torch.float64):
-        return torch.as_tensor(np.ascontiguousarray(x), dtype=dtype, device=dev)
-    t_pinfo, t_ainfo = dt(pinfo, torch.int32), dt(ainfo, torch.int32)
-    t_pprim, t_eab = dt(pprim), dt(eab)
-    lmax = max(s.l for s in sh)
-    cart = torch.zeros((ncart_tot, ncart_tot), dtype=torch.float64, device=dev)
-    tp, sel = _pair_sph(mol, prow, ncart_tot)
-    with torch.cuda.device(dev):
-        st = torch.cuda.current_stream(dev).cuda_stream
-        _capi.check(L.xt_int3c2e_cart(len(prow), t_pinfo.data_ptr(), t_pprim.data_ptr(), t_eab.data_ptr(),
-                                      len(prow), t_ainfo.data_ptr(), t_pprim.data_ptr(), t_eab.data_ptr(),
-                                      lmax, 2 * lmax, float(omega), cart.data_ptr(), ncart_tot, ctypes.c_void_p(st)),
-                    "xt_int3c2e_cart (4-index)")
-        t_tp = dt(tp)
-        s_ = _mm(L, st, dev, _mm(L, st, dev, t_tp, cart), t_tp, tb=1)          # (nsph_tot, nsph_tot)
-        # AO normalisation per pair row, then (ab|cd) = (cd|ab) exactly (the two come
-        # from different threads' summation orders): every symmetry copy is one element
-        w = np.zeros(s_.shape[0])
-        w[sel] = np.outer(mol._norm, mol._norm).ravel()
-        t_w = dt(w)
-        s_ *= t_w[:, None] * t_w[None, :]
-        s_ = 0.5 * (s_ + s_.t())
-        idx = dt(sel, torch.int64)
-        return s_.index_select(0, idx).index_select(1, idx).reshape(n, n, n, n).cpu().numpy()
+
+def _diag_blocks(tab, device, omega=0.0):
+    """Cartesian diagonal blocks (ab|ab) of every shell pair: (ncart_tot, maxnab)."""
+    torch = _torch()
+    L = _capi.lib()
+    d = tab.dev(device)
+    ldo = int(tab.nab.max())
+    kinfo = torch.as_tensor(tab.ket_info_pairs(np.arange(tab.npair), np.zeros(tab.npair, dtype=np.int32)),
+                            device=d["dev"])
+    out = torch.zeros((tab.ncart_tot, ldo), dtype=torch.float64, device=d["dev"])
+    _launch(L, tab, d, tab.npair, kinfo, d["pprim"], d["eab"], 2 * tab.lmax, omega, out, ldo, device, diag=1)
+    return out
+
+
+def eri_diag_device(mol, device: int = 0, omega: float = 0.0):
+    """(diag, q): the packed ERI diagonal (mu nu|mu nu), mu >= nu, (npack,) and the
+    per-shell-pair Schwarz bound q[k] >= |(mu nu|la si)| / q[k'] for normalised
+    spherical AOs of pairs k, k' (device tensors)."""
+    torch = _torch()
+    tab = pair_table(mol)
+    d = tab.dev(device)
+    dv = d["dev"]
+    with torch.cuda.device(dv):
+        blk = _diag_blocks(tab, device, omega)
+        dsph = torch.empty(tab.nsph_tot, dtype=torch.float64, device=dv)
+        q = torch.empty(tab.npair, dtype=torch.float64, device=dv)
+        wmax = torch.zeros(tab.npair, dtype=torch.float64, device=dv)
+        wmax.scatter_reduce_(0, torch.as_tensor(np.repeat(np.arange(tab.npair), tab.nsab), device=dv),
+                             d["wrow"], reduce="amax")
+        for Tk, cidx, sidx, ks in d["classes"]:
+            nc = cidx.shape[1]
+            b = blk[cidx][:, :, :nc]                                          # (npc, nc, nc)
+            dsph[sidx.reshape(-1)] = torch.einsum('sa,kab,sb->ks', Tk, b, Tk).reshape(-1)
+            cmax = torch.diagonal(b, dim1=1, dim2=2).clamp(min=0).amax(dim=1)
+            q[torch.as_tensor(ks, device=dv)] = torch.sqrt(cmax) * Tk.abs().sum(1).max()
+        dsph *= d["wrow"] ** 2
+        q *= wmax
+        return dsph[d["upack"]], q
+
+
+def eri_columns_device(mol, kets, q=None, thr: float = 0.0, device: int = 0, omega: float = 0.0):
+    """Columns (all packed pairs | packed pairs of shell pairs ``kets``):
+    returns (packed column indices (m,), (npack, m) tensor).  With Schwarz bounds
+    ``q`` (eri_diag_device) blocks whose bound is below ``thr`` are skipped."""
+    torch = _torch()
+    L = _capi.lib()
+    tab = pair_table(mol)
+    d = tab.dev(device)
+    dv = d["dev"]
+    kets = np.asarray(kets, dtype=np.int64)
+    nab = tab.nab[kets]
+    ncol = int(nab.sum())
+    kinfo = torch.as_tensor(tab.ket_info_pairs(kets), device=dv)
+    with torch.cuda.device(dv):
+        cart = torch.zeros((tab.ncart_tot, ncol), dtype=torch.float64, device=dv)
+        qk = None if q is None else q[torch.as_tensor(kets, device=dv)].contiguous()
+        _launch(L, tab, d, len(kets), kinfo, d["pprim"], d["eab"], 2 * tab.lmax, omega, cart, ncol, device,
+                qb=q, qk=qk, thr=thr)
+        rows = tab.rows_to_sph(cart, device)[d["upack"]]                    # (npack, ncol) packed rows
+        del cart
+        # ket side: Cartesian -> spherical per ket pair, keep the unique (mu >= nu) columns
+        cols, blocks = [], []
+        c = 0
+        for k, nc in zip(kets, nab):
+            i, j = tab.pairs[k]
+            si, sj = mol.shells[i], mol.shells[j]
+            Tk = torch.as_tensor(np.kron(_sph_transform(si.l), _sph_transform(sj.l)), device=dv)
+            mu = mol.ao_loc[i] + np.arange(si.nsph)[:, None]
+            nu = mol.ao_loc[j] + np.arange(sj.nsph)[None, :]
+            keep = (mu >= nu).ravel()
+            w = (mol._norm[mu] * mol._norm[nu]).ravel()[keep]
+            blk = torch.matmul(rows[:, c:c + nc], Tk.T)[:, torch.as_tensor(np.where(keep)[0], device=dv)]
+            blocks.append(blk * torch.as_tensor(w, device=dv)[None, :])
+            mm = np.broadcast_to(mu, (si.nsph, sj.nsph)).ravel()[keep]
+            nn = np.broadcast_to(nu, (si.nsph, sj.nsph)).ravel()[keep]
+            cols.append(mm * (mm + 1) // 2 + nn)
+            c += nc
+        return np.concatenate(cols), torch.cat(blocks, dim=1)
+
+
+# ---------------------------------------------------------------- 1-electron
+def int1e_nuc_device(mol, device: int = 0):
+    """Nuclear attraction sum_C -Z_C <mu|1/|r - C||nu> (PySCF int1e_nuc) on the GPU."""
+    torch = _torch()
+    L = _capi.lib()
+    tab = pair_table(mol)
+    d = tab.dev(device)
+    dv = d["dev"]
+    natm = mol.natm
+    s = POINT_CHARGE_EXP
+    kinfo = np.zeros((natm, 8), dtype=np.int32)
+    kinfo[:, 1] = 1
+    kinfo[:, 2] = np.arange(natm)
+    kinfo[:, 3] = np.arange(natm)
+    kinfo[:, 4] = np.arange(natm)
+    kinfo[:, 5] = 1
+    kprim = np.column_stack([np.full(natm, s), mol.atom_coords()])
+    ek = -mol._charges * (s / np.pi) ** 1.5
+    with torch.cuda.device(dv):
+        cart = torch.zeros((tab.ncart_tot, natm), dtype=torch.float64, device=dv)
+        _launch(L, tab, d, natm, torch.as_tensor(kinfo, device=dv), torch.as_tensor(kprim, device=dv),
+                torch.as_tensor(ek, device=dv), 0, 0.0, cart, natm, device)
+        v = tab.rows_to_sph(cart.sum(1, keepdim=True).contiguous(), device)[:, 0]
+        n = mol.nao
+        return v[d["sel"]].reshape(n, n).cpu().numpy()
+
+
+# ---------------------------------------------------------------- AO on the grid
+_SPH_TAB = None
+
+
+def _sph_table():
+    global _SPH_TAB
+    if _SPH_TAB is None:
+        _SPH_TAB = np.concatenate([_sph_transform(l).ravel() for l in range(AO_MAX_L + 1)])
+    return _SPH_TAB
+
+
+def ao_shell_tables(mol):
+    """(shell_info (nshell, 8) int32, shell_data) for xt_eval_ao."""
+    info, dat = [], []
+    off = 0
+    for s, p0 in zip(mol.shells, mol.ao_loc[:-1]):
+        if s.l > AO_MAX_L:
+            raise ValueError(f"xt_eval_ao handles l <= {AO_MAX_L}, got {s.l}")
+        info.append([s.l, s.exps.size, off, int(p0), 0, 0, 0, 0])
+        dat.append(np.concatenate([s.exps, s.coefs, s.center]))
+        off += 2 * s.exps.size + 3
+    return np.array(info, dtype=np.int32), np.concatenate(dat)
+
+
+def eval_ao_device(mol, coords, deriv: int = 0, device: int = 0, out=None, block: int = 1 << 17):
+    """AO values (deriv 0: (ngrid, nao)) or values + gradients (deriv 1:
+    (4, ngrid, nao)) on the GPU as a device tensor; evaluated in grid blocks of
+    ``block`` points into one resident array (or ``out``)."""
+    torch = _torch()
+    L = _capi.lib()
+    dv = torch.device(f"cuda:{device}")
+    c = coords if isinstance(coords, torch.Tensor) else torch.as_tensor(np.ascontiguousarray(coords), device=dv)
+    c = c.to(dv, torch.float64).contiguous()
+    ng, n = c.shape[0], mol.nao
+    ncomp = 4 if deriv else 1
+    info, dat = ao_shell_tables(mol)
+    with torch.cuda.device(dv):
+        t_info = torch.as_tensor(info, device=dv)
+        t_dat = torch.as_tensor(dat, device=dv)
+        t_sph = torch.as_tensor(_sph_table(), device=dv)
+        t_nrm = torch.as_tensor(mol._norm, device=dv)
+        if out is None:
+            out = torch.empty((ncomp, ng, n), dtype=torch.float64, device=dv)
+        st = _stream(device)
+        for g0 in range(0, ng, block):
+            g1 = min(ng, g0 + block)
+            _capi.check(L.xt_eval_ao(g1 - g0, c[g0:g1].data_ptr(), len(mol.shells), t_info.data_ptr(),
+                                     t_dat.data_ptr(), t_sph.data_ptr(), t_nrm.data_ptr(), int(bool(deriv)),
+                                     out[0, g0:g1].data_ptr(), n, ng * n, st), "xt_eval_ao")
+    return out if deriv else out[0]

@@ -253,10 +253,16 @@ class Mole:
         """PySCF ``Mole.intor_symmetric`` (the one-electron integrals here are all hermitian)."""
         return self.intor(name, comp=comp, origin=origin)
 
-    def intor(self, name: str, comp=None, hermi=0, origin=(0.0, 0.0, 0.0)):
+    def intor(self, name: str, comp=None, hermi=0, origin=(0.0, 0.0, 0.0), device=None):
         """PySCF names: int1e_ovlp, int1e_kin, int1e_nuc, int1e_r, int1e_ipovlp,
-        int1e_cg_irxp (comp 3; common gauge origin = ``origin``, PySCF's default 0), int2e."""
+        int1e_cg_irxp (comp 3; common gauge origin = ``origin``, PySCF's default 0), int2e.
+        ``device=k``: int1e_nuc and int2e through the GPU integral kernel (``qc.dints``)."""
         key = name.replace("_sph", "")
+        if device is not None and key == "int1e_nuc":
+            from .dints import int1e_nuc_device
+            return int1e_nuc_device(self, device)
+        if device is not None and key == "int2e":
+            return self.eri_full(device=device)
         if key == "int1e_ovlp":
             return self._intor_raw("ovlp")
         if key == "int1e_kin":
@@ -367,8 +373,13 @@ class Mole:
         return eri
 
     # ----------------------------------------------------- AO on the grid
-    def eval_ao(self, coords: np.ndarray, deriv: int = 0) -> np.ndarray:
-        """AO values (deriv 0: (ngrid, nao)) or values + gradients (deriv 1: (4, ngrid, nao))."""
+    def eval_ao(self, coords: np.ndarray, deriv: int = 0, device=None):
+        """AO values (deriv 0: (ngrid, nao)) or values + gradients (deriv 1: (4, ngrid, nao)).
+        ``device=k``: evaluated on GPU k in grid blocks (``xt_eval_ao``), returned as a
+        device tensor that stays in HBM."""
+        if device is not None:
+            from .dints import eval_ao_device
+            return eval_ao_device(self, coords, deriv, device)
         coords = np.asarray(coords, dtype=np.float64)
         ng = coords.shape[0]
         ncomp = 4 if deriv else 1

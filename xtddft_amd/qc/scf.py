@@ -30,6 +30,7 @@ from .grid import gen_grids
 from .gto import C2V_IRREPS
 
 XC_BLOCK = 16384
+INCORE_MAX_NAO = 200      # eri_mode 'auto' on a GPU: stored ERIs up to this size, Cholesky above
 
 
 class _SCFBase:
@@ -50,6 +51,10 @@ class _SCFBase:
         self.scf_summary = {}
         self.mo_coeff = self.mo_occ = self.mo_energy = None
         self.with_df = None
+        self.eri_mode = "auto"          # 'incore' | 'cholesky' | 'auto' (see build)
+        self.chol_tol = 1e-12
+        self.cderi_exact = None
+        self.timings = {}
         self.device_engine = None
         self._device = None
         self._built = False
@@ -74,23 +79,60 @@ class _SCFBase:
         self._built = False
         return self
 
+    def cholesky(self, tol: float = 1e-12):
+        """Exact J/K from the integral-direct pivoted Cholesky factor of the ERIs,
+        computed on the GPU without the 4-index array (``qc.dchol``; the direct-SCF
+        mean field the reference defaults to, XTDA.py:518-543).  Needs to_device()."""
+        self.eri_mode = "cholesky"
+        self.chol_tol = float(tol)
+        self._built = False
+        return self
+
+    def _use_cholesky(self):
+        if self.with_df is not None:
+            return False
+        if self.eri_mode == "cholesky":
+            if self._device is None:
+                raise ValueError("the integral-direct Cholesky factor is computed on the GPU: call to_device() first")
+            return True
+        return self.eri_mode == "auto" and self._device is not None and self.mol.nao > INCORE_MAX_NAO
+
     # ----------------------------------------------------------- set-up
     def build(self):
         if self._built:
             return self
+        import time
         mol = self.mol
+        dev = getattr(self, "_device", None)
         self.comps, self.hyb, self.xctype = _xc.parse_xc(self.xc)
+        t0 = time.perf_counter()
         self.s1e = mol.intor("int1e_ovlp")
-        self.h1e = mol.intor("int1e_kin") + mol.intor("int1e_nuc")
-        self.eri = mol.eri_full(device=getattr(self, "_device", None)) if self.with_df is None else None
-        if self.with_df is not None:
+        self.h1e = mol.intor("int1e_kin") + mol.intor("int1e_nuc", device=dev)
+        self.timings["int1e_s"] = time.perf_counter() - t0
+        self.eri = None
+        self._eri_k = None
+        self.cderi_exact = None
+        t0 = time.perf_counter()
+        if self._use_cholesky():
+            from .dchol import cholesky_eri
+            st = {}
+            self.cderi_exact = cholesky_eri(mol, self.chol_tol, dev, stats=st)
+            self.timings["cholesky"] = st
+        elif self.with_df is None:
+            self.eri = mol.eri_full(device=dev)
+        else:
             self.with_df.build()
+        self.timings["int2e_s"] = time.perf_counter() - t0
         if self.xctype != "HF":
+            t0 = time.perf_counter()
             if self.grids is None:
                 self.grids = gen_grids(mol)
-            self.ao = mol.eval_ao(self.grids.coords, deriv=1 if self.xctype == "GGA" else 0)
+            self.timings["grid_s"] = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            self.ao = mol.eval_ao(self.grids.coords, deriv=1 if self.xctype == "GGA" else 0, device=dev)
             if self.ao.ndim == 2:
                 self.ao = self.ao[None]
+            self.timings["eval_ao_s"] = time.perf_counter() - t0
         if self._device is not None:
             from .device import DeviceEngine
             self.device_engine = DeviceEngine(self, self._device)
@@ -522,6 +564,9 @@ def _meanfield(mf, chol_tol):
     if mf.with_df is not None:      # DF mean field: the fitted factor, no 4-index ERIs
         eri8 = None
         cderi = mf.with_df.cderi
+    elif mf.cderi_exact is not None:   # integral-direct Cholesky: the exact factor, on the device
+        eri8 = None
+        cderi = mf.cderi_exact
     else:
         eri8 = pack_s8(mf.eri)
         cderi = pivoted_cholesky(mf.eri.reshape(nao * nao, nao * nao), chol_tol).reshape(-1, nao, nao)
@@ -541,7 +586,7 @@ def _meanfield(mf, chol_tol):
             rho0[:, 0] = rho[:, 0]
             vxc0 = _xc.eval_xc_eff(mf.xc, rho0, deriv=1)[1]
             fxc_sf = (vxc0[0, 0] * w - vxc0[1, 0] * w) / (rho[0, 0] - rho[1, 0] + 1e-9)
-        grids = Grid(ao=np.ascontiguousarray(ao), weights=np.ascontiguousarray(w))
+        grids = Grid(ao=ao if _is_tensor(ao) else np.ascontiguousarray(ao), weights=np.ascontiguousarray(w))
     mfmol = MFMole(nao=nao, spin=mol.spin, nelectron=mol.nelectron, symmetry=mol.symmetry is not None)
     out = MeanField(mol=mfmol, mo_coeff=mf.mo_coeff, mo_occ=mf.mo_occ, mo_energy=mf.mo_energy,
                     h1e=mf.h1e, veff=np.asarray(mf._veff), veff_hf=np.asarray(veff_hf),
@@ -552,6 +597,10 @@ def _meanfield(mf, chol_tol):
     if not mf.restricted_open:
         out.extra["spin_square"] = mf.spin_square()
     return out
+
+
+def _is_tensor(x):
+    return type(x).__module__.startswith("torch")
 
 
 def as_device_eri8(mfield):
