@@ -97,7 +97,7 @@ def parse(argv=None):
     ap.add_argument("--jk", default=None, choices=["DF", "ERI8"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-converge", action="store_true")
-    ap.add_argument("--converge", action="store_true", help="also at N > 1")
+    ap.add_argument("--converge", action="store_true", help="force the Davidson run (default on; see --no-converge)")
     ap.add_argument("--k-mode", default="auto", choices=["auto", "direct", "stored"],
                     help="exchange evaluation (xt_set_exchange_mode)")
     args = ap.parse_args(argv)
@@ -393,16 +393,20 @@ def converge(args, w, allreduce):
         kw = dict(tol=1e-8, lindep=1e-9, max_cycle=1000)
         pre = DiagPrecond(hdiag, 1e-3, dev.index)
         crit = "tol 1e-8, lindep 1e-9 (XSF_TDA.py:1467-1470)"
-    stats = dict(calls=0, vectors=0, s=0.0)
+    stats = dict(calls=0, vectors=0, s=0.0, allreduce_s=0.0, nvec=[])
 
     def aop(xt):
         t = time.perf_counter()
         s = op.apply(xt)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
         allreduce(s)
         torch.cuda.synchronize()
         stats["calls"] += 1
         stats["vectors"] += int(s.shape[0])
-        stats["s"] += time.perf_counter() - t
+        stats["nvec"].append(int(s.shape[0]))
+        stats["s"] += t1 - t
+        stats["allreduce_s"] += time.perf_counter() - t1
         return s
     torch.cuda.synchronize()
     log(f"converging {args.nroots} roots")
@@ -411,10 +415,16 @@ def converge(args, w, allreduce):
                                  return_device=True, **kw)
     torch.cuda.synchronize()
     wall = time.perf_counter() - tc
+    hist = {}
+    for k in stats["nvec"]:
+        hist[k] = hist.get(k, 0) + 1
     return dict(nroots=args.nroots, wall_s=round(wall + w.t_op, 2), davidson_s=round(wall, 2),
                 operator_setup_s=round(w.t_op, 2), iterations=int(icyc) + 1,
                 converged=bool(np.all(conv)), ax_calls=stats["calls"], ax_vectors=stats["vectors"],
-                ax_s=round(stats["s"], 2), e_min_ha=float(e[0]), criteria=crit)
+                ax_s=round(stats["s"], 3), allreduce_s=round(stats["allreduce_s"], 3),
+                host_davidson_s=round(wall - stats["s"] - stats["allreduce_s"], 3),
+                nvec_histogram={str(k): v for k, v in sorted(hist.items())},
+                e_min_ha=float(e[0]), criteria=crit)
 
 
 # ---------------------------------------------------------------------------
@@ -452,6 +462,26 @@ def roofline_of(args, stats_acc, steps, world=1):
                 frac=round(achieved / FP64_PEAK_TFLOPS, 4), traffic=traffic,
                 kernel=dom_name, avg_launch_ms=round(avg_ms, 4),
                 flops_per_launch=flops_launch, launches_per_step=dom["launches"] / steps)
+
+
+def breakdown(op, z, out, allreduce, sync, stats_acc, steps, rank, world, reps=2):
+    """This rank's phase split of one step: device A.x and the sigma all-reduce each
+    timed between synchronisations (``reps`` extra steps after the timed region), and
+    the live per-class kernel ms of the timed steps."""
+    ta = tr = 0.0
+    for _ in range(reps):
+        sync()
+        t0 = time.perf_counter()
+        op.apply(z, out)
+        sync()
+        t1 = time.perf_counter()
+        allreduce(out)
+        sync()
+        ta += t1 - t0
+        tr += time.perf_counter() - t1
+    return dict(rank=rank, ax_ms=round(1e3 * ta / reps, 3), allreduce_ms=round(1e3 * tr / reps, 3),
+                sigma_mb=round(out.numel() * 8 / 1e6, 3),
+                kernel_ms={k: round(v["ms"] / steps, 3) for k, v in stats_acc.items() if v["launches"]})
 
 
 def rank_main(args):
@@ -526,6 +556,8 @@ def rank_main(args):
     log(f"timed {args.steps} steps: {1e3 * T / args.steps:.2f} ms per step")
     verify = w.verify(z, out) if hasattr(w, "verify") else None   # a workload's own self-check
     phases = op.last_timings()
+    # per-rank breakdown (outside the timed region: synchronised after each phase)
+    mine = breakdown(op, z, out, allreduce_sigma, sync, stats_acc, args.steps, rank, world)
     roofline = roofline_of(args, stats_acc, args.steps, world)
     others = {}
     for k, v in stats_acc.items():
@@ -569,8 +601,15 @@ def rank_main(args):
             result["cpu_baseline"] = cpu_baseline(args)
         except Exception as e:   # report, never hide
             result["cpu_baseline"] = dict(value=None, error=repr(e))
-    if use_gpu and ((world == 1 and not args.no_converge) or args.converge):
+    if use_gpu and (not args.no_converge or args.converge):
         result["converge"] = converge(args, w, allreduce_sigma)
+        mine["converge"] = {k: result["converge"][k] for k in ("ax_s", "allreduce_s", "host_davidson_s")}
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+        result["ranks"] = ranks
+    else:
+        result["ranks"] = [mine]
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -9,23 +9,28 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_bench_self_launches_two_ranks():
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_self_launches_ranks(world):
     env = dict(os.environ, XT_BENCH_BACKEND="gloo", XT_BENCH_OPERATOR="bench_stub:make_workload",
                PYTHONPATH=os.path.join(ROOT, "tests") + os.pathsep + ROOT, OMP_NUM_THREADS="1")
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
            "--nao", "24", "--nclosed", "5", "--nopen", "2", "--naux", "40", "--ngrid", "600", "--nvec", "3"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout       # rank 0 only
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["n_gpus"] == world and d["steps"] == 2 and d["warmup"] == 1
     assert d["scaling"] == "strong" and d["value"] > 0
     assert d["verify"] < 1e-12, d["verify"]   # all-reduced shard sums == full operator
     assert "STUB" in d["data"]
-
-
-import pytest  # noqa: E402
+    # per-rank phase split from every rank
+    assert [x["rank"] for x in d["ranks"]] == list(range(world))
+    for x in d["ranks"]:
+        assert x["ax_ms"] > 0 and x["allreduce_ms"] >= 0 and x["sigma_mb"] > 0
 
 
 @pytest.mark.gpu
@@ -46,3 +51,4 @@ def test_bench_two_ranks_on_the_gpu():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["value"] > 0 and "STUB" not in d["data"]
     assert "grid sharded x2" in d["config"]["parallelism"]
+    assert len(d["ranks"]) == 2 and all(x["ax_ms"] > 0 for x in d["ranks"])

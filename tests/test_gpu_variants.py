@@ -1,20 +1,16 @@
-"""GPU: the alternative kernel paths each context can select (environment, read at
-xt_create) against the oracle, and the XSF exchange through the stored matrix at
-the row counts that take its 160-row streaming tile and its batching.
+"""GPU: the kernel paths each context selects for the fused XC classes, against the
+oracle, and the XSF exchange through the stored matrix at the row counts that take
+its 160-row streaming tile and its batching.
 
-* XT_M_KERNEL=0  -> XC M-backward through the generic engine's mode 2
-  (default: the dedicated kernel, xt_xcm.hip)
-* XT_W_KERNEL=0  -> XC rho-forward through the generic engine's mode 1
-  (default: the dedicated kernel, xt_xcw.hip)
-* XT_W_RING=0    -> the dedicated rho-forward kernel's select-based ring advance
-* XT_M_WAB=0     -> dedicated M-backward with the next K-tile's LDS writes before the
-  closing barrier (default: after the opening one)
-* XT_W_TNG=2 / XT_W_XW=2 -> dedicated rho-forward on 32-point blocks / with two trial
-  pairs per wave (default: 64-point blocks of eight one-pair waves)
-* XT_XSF_FUSED=0 -> XSF Delta-A exchange as direct DF sandwiches
-  (default with the stored exchange: one Kx stream for main + Delta-A exchange)
-* XT_SKINNY_RV=0 -> 33..40-row stored exchange through the 48-row MFMA tile
-  (default: 32 MFMA rows + up to 8 VALU remainder rows)
+Automatic selection (xt_ctx.hip): the dedicated M-backward kernel (xt_xcm.hip) for
+O <= 128 and the generic engine's fused mode 2 above; the dedicated rho-forward
+kernel (xt_xcw.hip) for O >= 96 and the engine's fused mode 1 below, where it wins.
+The two test hooks (environment, read once at xt_create) force either side outside
+its automatic range so each path is checked at every occupied-row shape:
+
+* XT_M_KERNEL=0 -> XC M-backward through the engine's mode 2
+* XT_W_KERNEL=0 / 1 -> XC rho-forward through the engine's mode 1 / the dedicated kernel
+
 Tolerance: 1e-12 relative max-norm on sigma (FP64 round-off of a different
 summation order), as in test_gpu_parity.py.
 """
@@ -51,12 +47,8 @@ def env():
             os.environ[k] = v
 
 
-@pytest.mark.parametrize("knobs", [dict(XT_M_KERNEL=0), dict(XT_W_KERNEL=0), dict(XT_M_KERNEL=0, XT_W_KERNEL=0),
-                                   dict(XT_M_KERNEL=1, XT_W_KERNEL=1), dict(XT_W_RING=0),
-                                   dict(XT_M_WAB=0), dict(XT_W_KERNEL=1, XT_W_TNG=2, XT_W_XW=2),
-                                   dict(XT_W_KERNEL=1, XT_W_TNG=2), dict(XT_W_KERNEL=1, XT_W_XW=2),
-                                   dict(XT_W_KERNEL=1, XT_W_TNG=2, XT_W_XW=2, XT_W_RING=0),
-                                   dict(XT_W_KERNEL=1, XT_W_ZD=6), dict(XT_W_KERNEL=1, XT_W_ORDER=1)])
+@pytest.mark.parametrize("knobs", [dict(), dict(XT_M_KERNEL=0), dict(XT_W_KERNEL=0), dict(XT_M_KERNEL=0, XT_W_KERNEL=0),
+                                   dict(XT_M_KERNEL=1, XT_W_KERNEL=1)])
 @pytest.mark.parametrize("nc,no,nao", [(5, 2, 26), (33, 1, 60), (35, 2, 70), (95, 2, 130), (99, 2, 140),
                                       (120, 3, 150)])
 def test_xc_kernel_variants(hiplib, env, knobs, nc, no, nao):
@@ -73,11 +65,9 @@ def test_xc_kernel_variants(hiplib, env, knobs, nc, no, nao):
 
 @pytest.mark.parametrize("nz", [13, 41])
 @pytest.mark.parametrize("sa", [2, 3])
-@pytest.mark.parametrize("fused", [1, 0])
-def test_xsf_stored_exchange_blocks(hiplib, env, nz, sa, fused):
+def test_xsf_stored_exchange_blocks(hiplib, nz, sa):
     """4 nz = 52 rows (160-row tile) and 41 vectors (one 40-vector batch + 1)."""
     from xtddft_amd.operator import DeviceOperator
-    env(XT_XSF_FUSED=fused)
     mf = make_mf(nao=30, nc=6, no=3, xctype="GGA", hyb=0.5)
     o = oxsf.XSFOracle(mf, SA=sa)
     fg = oxsf.default_fglobal(mf)
@@ -88,13 +78,11 @@ def test_xsf_stored_exchange_blocks(hiplib, env, nz, sa, fused):
     assert rel(op.apply(z), vind(z)) < RTOL
 
 
-@pytest.mark.parametrize("nz", [17, 20])
-@pytest.mark.parametrize("rv", [1, 0])
-def test_stored_exchange_row_shapes(hiplib, env, nz, rv):
+@pytest.mark.parametrize("nz", [17, 20, 23])
+def test_stored_exchange_row_shapes(hiplib, nz):
     """2 nz = 34 / 40 rows: the 32 MFMA rows + VALU remainder shape of the streaming
-    exchange kernel (XT_SKINNY_RV=1, default) and the 48-row MFMA shape."""
+    exchange kernel; 46 rows: the 48-row MFMA shape."""
     from xtddft_amd.operator import DeviceOperator
-    env(XT_SKINNY_RV=rv)
     mf = make_mf(nao=40, nc=8, no=2, ngrid=2000, xctype="GGA", hyb=0.25)
     vind, hdiag = oxtda.gen_tda_operation(mf)
     z = make_trial_vectors(nz, hdiag.size)

@@ -94,10 +94,8 @@ struct xt_ctx {
   // rank partition (xt_set_partition): aux window for J / direct exchange / XSF
   // Delta-A over the resident factor, and the occupied rows of the stored exchange
   int win_p0 = 0, win_np = -1;   // -1: all aux rows
-  bool skinny = true;            // stored exchange through the skinny streaming kernel (XT_SKINNY=0: generic tile)
   bool m_kernel = true;          // XC M-backward through xt_xcm.hip (XT_M_KERNEL=0: the engine's mode 2)
   int w_kernel = 2;              // XC rho-forward: 1 xt_xcw.hip, 0 the engine's mode 1, 2 by size (XT_W_KERNEL)
-  bool xsf_fused = true;         // XSF Delta-A exchange through the stored matrix (XT_XSF_FUSED=0: direct)
   int kr0 = 0, kr1 = -1;         // -1: all O rows
 };
 
@@ -236,14 +234,14 @@ int xt_create(const xt_desc* desc, xt_ctx** out) {
   }
   for (int i = 0; i < 5; ++i) (void)hipEventCreate(&c->ev[i]);
   {
-    const char* e = getenv("XT_SKINNY");
-    c->skinny = !(e && atoi(e) == 0);
+    // the only environment knobs, read here once per context: which XC kernels run the
+    // fused classes outside their automatic ranges (tests/test_gpu_variants.py).
+    // Defaults: dedicated M-backward for O <= 128 and rho-forward for O >= 96, the
+    // engine's fused modes otherwise (where they win or the dedicated kernels do not fit)
     const char* em = getenv("XT_M_KERNEL");
     c->m_kernel = !(em && atoi(em) == 0);
     const char* ew = getenv("XT_W_KERNEL");
     c->w_kernel = ew ? (atoi(ew) == 0 ? 0 : 1) : 2;
-    const char* ex = getenv("XT_XSF_FUSED");
-    c->xsf_fused = !(ex && atoi(ex) == 0);
   }
   *out = c;
   return 0;
@@ -851,7 +849,7 @@ static int exchange_stored(xt_ctx* c, int nz) {
     const double* A = c->ze.p + gr[q].ch0 * chs + (long)i0 * c->V;
     const double* B = c->Kx.p + (size_t)q * blk;
     double* C = c->acc.p + gr[q].ch0 * chs;
-    if (M <= SKINNY_MAX_M && c->skinny) {
+    if (M <= SKINNY_MAX_M) {
       bool prof = false;
       RET(prof_begin(c, 1, 2.0 * M * (double)ov * K, 8.0 * ((double)ov * K + (double)M * K + 2.0 * M * (double)ov), &prof));
       const size_t need = skinny_workspace_bytes(M, (int)ov, K);
@@ -883,7 +881,7 @@ static int exchange_stored(xt_ctx* c, int nz) {
 static bool xsf_fused_k(const xt_ctx* c) {
   const xt_desc& d = c->d;
   return d.kind == XT_KIND_XSF && d.sa > 1 && c->k_resolved == 1 && c->ck != 0.0 && c->ck_lr == 0.0 &&
-         c->nchan == 1 && c->xsf_fused;
+         c->nchan == 1;
 }
 
 static int exchange_stored_xsf(xt_ctx* c, int nz) {

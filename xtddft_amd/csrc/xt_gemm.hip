@@ -628,20 +628,10 @@ static void launch_one(const GemmParams& p, hipStream_t st) {
                      dim3(tiles, 1, p.nbatch * p.nsplit), dim3(64 * WGM * WGN), 0, st, p);
 }
 
-// Tuning knobs (environment, read once): XT_W_BN=128 runs the fused rho-forward
-// GEMM on 128-point grid tiles (one block per CU); XT_M_MAP=0 restores the old
-// mode-2 staging map.
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
-// mode 2 tile width: 64 (BK 16, two blocks per CU) or, with XT_M_BN=128, 128 (BK 32,
-// 8 xg x 16 a per column tile, one block per CU)
-int xc_m_bn() {
-  static const int bn = env_int("XT_M_BN", 64) == 128 ? 128 : 64;
-  return bn;
-}
+// Engine shapes measured and removed: mode 1 on 128-point grid tiles
+// (one block per CU), mode 2 on a 128-wide column tile (BK 32) and with the old
+// staging map (2-way ds_write_b64 conflicts).
+int xc_m_bn() { return 64; }
 
 // Tagged call sites get their own kernel symbol for their one operand layout:
 // 1 exchange contraction (A k-contig, B n-contig), 2 XC forward U (k, k),
@@ -665,17 +655,6 @@ size_t dgemm_workspace_bytes(const GemmDesc& d) {
   plan_gemm(d, &p, &cfg);
   if (p.nsplit <= 1) return 0;
   return sizeof(double) * (size_t)p.nsplit * p.nbatch * (size_t)p.M * p.N;
-}
-
-// Debug / tuning knob: XT_GEMM_CFG=<index into kCfg> forces a configuration.
-static int forced_cfg() {
-  static int v = -2;
-  if (v == -2) {
-    const char* e = getenv("XT_GEMM_CFG");
-    v = e ? atoi(e) : -1;
-    if (v >= (int)(sizeof(kCfg) / sizeof(kCfg[0]))) v = -1;
-  }
-  return v;
 }
 
 // Relative MFMA time of a tile with vm valid rows / vn valid cols: the busiest
@@ -779,8 +758,7 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
   // the stored-exchange stream (skinny M, K = N = O V, HBM-bound): the 8-wave
   // two-blocks-per-CU tile keeps more loads in flight than 64x128 (21.4 -> 20.0 ms)
   if (d.tag == 1 && !ff && d.N >= 96) cfg = 5;
-  static const int rowsimd = env_int("XT_ROWSIMD", 1);
-  if (cfg == 5 && rowsimd && !(d.tag == 1 && !ff)) {
+  if (cfg == 5 && !(d.tag == 1 && !ff)) {
     // ragged column edge: rows on the SIMDs when that makes the edge tiles cheaper
     const int vm = d.M - ((d.M + 127) / 128 - 1) * 128, vn = d.N - ((d.N + 127) / 128 - 1) * 128;
     const long tm = (d.M + 127) / 128, tn = (d.N + 127) / 128;
@@ -790,7 +768,6 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
     };
     if (total(kCfg[8]) < 0.97 * total(kCfg[5])) cfg = 8;   // (model gains under 3 % measured neutral or worse)
   }
-  if (forced_cfg() >= 0) cfg = forced_cfg();
   const Cfg& c = kCfg[cfg];
   const long units = (long)p.R * ((d.K + c.bk - 1) / c.bk);
   int nsplit = choose_split(c, d.M, d.N, p.nbatch, units);
@@ -833,21 +810,11 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
     p.ws = ws;
   }
   if (mode == 1) {
-    static const int w_bn = env_int("XT_W_BN", 64);
-    if (w_bn == 128) launch_one<128, 128, 2, 4, 16, 2, false, true, 4, 1>(p, st);
-    else             launch_one<128, 64, 2, 4, 16, 4, false, true, 4, 1>(p, st);
+    launch_one<128, 64, 2, 4, 16, 4, false, true, 4, 1>(p, st);
   } else if (mode == 2) {
-    static const int m_map = env_int("XT_M_MAP", 1);
     // rows = occupied orbitals: a 64-row tile when they fit (small molecules)
-    if (d.fz.mbn == 128) {
-      launch_one<128, 128, 2, 4, 32, 2, false, true, 5, 2>(p, st);
-    } else if (m_map == 1) {
-      if (d.M <= 64) launch_one<64, 64, 2, 4, 16, 4, false, true, 5, 2, 1>(p, st);
-      else           launch_one<128, 64, 2, 4, 16, 4, false, true, 5, 2, 1>(p, st);
-    } else {
-      if (d.M <= 64) launch_one<64, 64, 2, 4, 16, 4, false, true, 5, 2>(p, st);
-      else           launch_one<128, 64, 2, 4, 16, 4, false, true, 5, 2>(p, st);
-    }
+    if (d.M <= 64) launch_one<64, 64, 2, 4, 16, 4, false, true, 5, 2, 1>(p, st);
+    else           launch_one<128, 64, 2, 4, 16, 4, false, true, 5, 2, 1>(p, st);
   } else switch (cfg) {
     case 0: launch_cfg<128, 128, 2, 4, 32, 2>(p, st, akc, bkc, d.tag); break;
     case 1: launch_cfg<128, 128, 2, 2, 16, 2>(p, st, akc, bkc, d.tag); break;

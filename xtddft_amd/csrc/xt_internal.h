@@ -20,7 +20,7 @@ namespace xt {
 //  mode 2 "M backward":   B(g, n) generated as sum_c rho[g rg + 3 xg + c] w[c wc + g wg + a]
 //    with n -> (xg, a) in (XC_M_BN / 16) x 16 blocks (xg-block fastest); C column xg V + a;
 //    N must be xc_m_cols(nx, V, mbn).
-int xc_m_bn();                // mode 2 column-tile width of the launched variant (64 or 128)
+int xc_m_bn();                // mode 2 column-tile width (64)
 inline int xc_m_cols(int nx, int V, int bn) {
   return ((nx + bn / 16 - 1) / (bn / 16)) * ((V + 15) / 16) * bn;
 }

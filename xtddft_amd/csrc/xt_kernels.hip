@@ -828,8 +828,7 @@ void xc_uks_w(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O
                        pO0, pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1);
 }
 void xc_sf(hipStream_t st, int G, int g0, int nz, int O, int nmo, const double* phio, const double* fsf, double* U) {
-  const char* e = getenv("XT_SF_POINT");
-  if (!(e && atoi(e) == 0) && O <= 256) {
+  if (O <= 256) {   // one wave per grid point; the wave-per-(point, vector) kernel beyond
     const dim3 grid((G + 3) / 4), blk(256);
     if (O <= 128)      hipLaunchKernelGGL((k_xc_sf_pt<2>), grid, blk, 0, st, G, g0, nz, O, nmo, phio, fsf, U);
     else if (O <= 192) hipLaunchKernelGGL((k_xc_sf_pt<3>), grid, blk, 0, st, G, g0, nz, O, nmo, phio, fsf, U);

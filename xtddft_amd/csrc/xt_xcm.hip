@@ -26,7 +26,6 @@
 // Split over the grid (K) for occupancy: each split writes its own slab, reduced in a
 // fixed order (deterministic) and added to accT.
 #include <hip/hip_runtime.h>
-#include <stdlib.h>
 #include "xt_internal.h"
 
 namespace xt {
@@ -35,17 +34,15 @@ namespace xt {
 typedef double d4m __attribute__((ext_vector_type(4)));
 
 constexpr int BM_AB = 32;        // virtuals per block (2 MFMA column sub-tiles per wave)
-// Block shapes (NW waves, one trial pair each; K-tile of 4 NW grid points):
-//   NW 8: 512 threads, 32-point K-tiles, one block per CU (118 KB LDS at TM 7)
-//   NW 4: 256 threads, 16-point K-tiles, two blocks per CU (59 KB each): the other
-//         block's MFMAs run through one block's barrier / staging phase
+constexpr int NW = 8;            // waves per block, one trial pair each: 512 threads,
+                                 // 32-point K-tiles, one block per CU (118 KB LDS at TM 7)
 
 // LDS images (doubles), one buffer:
 //   A  [g 32][i 16 TM]        swizzle i ^ 16 (g & 1) for even TM (odd TM: the row pitch
 //                             16 TM = 16 mod 32 doubles already separates the halves)
 //   W  [c 3][g 32][a 32]      swizzle a ^ 16 (g & 1)
 //   R  [g 32][xg 8][c 3]      (broadcast reads)
-template <int TM, int NW>
+template <int TM>
 struct BmLds {
   static constexpr int BK = 4 * NW, XB = NW;
   static constexpr int A = BK * 16 * TM;
@@ -71,14 +68,14 @@ __device__ __forceinline__ double rows4_m(double v) {
 // (TM - 1) + RV); those rows are accumulated on the VALU (RV x 2 FMAs per k-step
 // against the same B fragments, ~55 cycles at RV = 5) instead of a 16-row MFMA
 // sub-tile (2 MFMAs, ~145 cycles), and reduced over the four k-rows once per block.
-template <int TM, bool GEN_FIRST, int RV = 0, int NW = 8, bool WAB = false>
+template <int TM, int RV = 0>
 __global__ void __launch_bounds__(64 * NW, 1)
 k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
             const double* __restrict__ PO, long ldp,
             const double* __restrict__ Wg, long wc, long wg,
             const double* __restrict__ R, long rg,
             double* __restrict__ out, long ldo, long slab) {
-  using L = BmLds<TM, NW>;
+  using L = BmLds<TM>;
   constexpr int BM_BK = L::BK, BM_XB = L::XB, NT = 64 * NW;
   constexpr int R_LD = (L::R + NT - 1) / NT;
   constexpr int PA = 16 * TM;                  // A row length (i)
@@ -194,8 +191,8 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
   // below is a lane base plus a compile-time offset.
   // The B fragments of k-step s + 1 are generated before the MFMAs of step s in
   // program order (their LDS reads and the 3-deep FP64 chain then overlap step s's
-  // matrix work instead of stalling step s + 1's first MFMA); GEN_FIRST instead
-  // builds all 8 steps' fragments up front.
+  // matrix work instead of stalling step s + 1's first MFMA; building all 8 steps'
+  // fragments up front measured +4 %).
   const int swl = (q & 1) << 4;
   const int a_lane = q * PA + ((r16) ^ ((q & 1) * SWA));        // A: row q, column r16 (+16 t via XOR-free add)
   const int w_lane = L::A + q * BM_AB;                           // W: row q
@@ -236,28 +233,21 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
         for (int j = 0; j < 2; ++j)
           acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t], b[j], acc[t][j], 0, 0, 0);
     };
-    if constexpr (GEN_FIRST) {
-      double b[BM_BK / 4][2];
+    double b[2][2];
+    gen(0, b[0]);
 #pragma unroll
-      for (int ks = 0; ks < BM_BK / 4; ++ks) gen(ks, b[ks]);
-#pragma unroll
-      for (int ks = 0; ks < BM_BK / 4; ++ks) mma(ks, b[ks]);
-    } else {
-      double b[2][2];
-      gen(0, b[0]);
-#pragma unroll
-      for (int ks = 0; ks < BM_BK / 4; ++ks) {
-        if (ks + 1 < BM_BK / 4) gen(ks + 1, b[(ks + 1) & 1]);
-        mma(ks, b[ks & 1]);
-      }
+    for (int ks = 0; ks < BM_BK / 4; ++ks) {
+      if (ks + 1 < BM_BK / 4) gen(ks + 1, b[(ks + 1) & 1]);
+      mma(ks, b[ks & 1]);
     }
   };
   (void)a_lane;
 
-  if (WAB && kt0 < kt1) {
+  if (kt0 < kt1) {
     // K-tile kt + 1 is written to LDS right after the barrier that opens K-tile kt (its
     // buffer was last read by K-tile kt - 1) and kt + 2 is loaded right after: the
-    // stores overlap the other waves' MFMAs instead of delaying the barrier
+    // stores overlap the other waves' MFMAs instead of delaying the barrier (writing
+    // them before the closing barrier instead: +1 %)
     load(kt0);
     store(0, kt0);
     if (kt0 + 1 < kt1) load(kt0 + 1);
@@ -267,21 +257,6 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
       if (kt + 1 < kt1) store(buf ^ 1, kt + 1);
       if (kt + 2 < kt1) load(kt + 2);
       if (wave_on) compute(buf);
-      __syncthreads();
-      buf ^= 1;
-    }
-  } else if (kt0 < kt1) {
-    load(kt0);
-    store(0, kt0);
-    __syncthreads();
-    int buf = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const bool more = kt + 1 < kt1;
-      if (more) load(kt + 1);
-      if (wave_on) compute(buf);
-      // the LDS stores (and their vmcnt waits) stay behind every MFMA of this tile
-      __builtin_amdgcn_sched_barrier(0);
-      if (more) store(buf ^ 1, kt + 1);
       __syncthreads();
       buf ^= 1;
     }
@@ -341,22 +316,15 @@ static int back_m_splits(int tiles, int nkt, int slots) {
   return best;
 }
 
-// block shape: XT_M_NW=4 selects the 4-wave, two-blocks-per-CU shape (measured
-// 167.7 vs 161.4 ms/step for the 8-wave shape on the same box: hiding one block's
-// barrier under the other's MFMAs does not pay for twice the barriers and A-tile loads)
-static int back_m_nw() {
-  const char* e = getenv("XT_M_NW");
-  return (e && atoi(e) == 4) ? 4 : 8;
-}
-
-struct BackMPlan { int nw, tiles, nkt, splits, kps, used, blocks; };
+// (a 4-wave, two-blocks-per-CU shape measured 167.7 vs 161.4 ms/step: hiding one
+// block's barrier under the other's MFMAs did not pay for twice the barriers and loads)
+struct BackMPlan { int tiles, nkt, splits, kps, used, blocks; };
 static BackMPlan back_m_plan(int nx, int V, int n) {
   BackMPlan p;
-  p.nw = back_m_nw();
-  const int bk = 4 * p.nw, xb = p.nw;
+  const int bk = 4 * NW, xb = NW;
   p.tiles = ((nx + xb - 1) / xb) * ((V + BM_AB - 1) / BM_AB);
   p.nkt = (n + bk - 1) / bk;
-  p.splits = back_m_splits(p.tiles, p.nkt, p.nw == 4 ? 512 : 256);
+  p.splits = back_m_splits(p.tiles, p.nkt, 256);
   p.kps = (p.nkt + p.splits - 1) / p.splits;
   p.used = (p.nkt + p.kps - 1) / p.kps;
   p.blocks = p.tiles * p.used;
@@ -368,61 +336,25 @@ size_t xc_back_m_workspace_bytes(int O, int nx, int V, int n) {
   return sizeof(double) * (size_t)p.splits * O * (size_t)nx * V;
 }
 
-template <int TM, int RV, int NW>
-static void launch_back_m_rv(int O, int nx, int V, int n, int kps, int blocks, const double* PO, long ldp,
-                             const double* W, long wc, long wg, const double* R, long rg, double* ws, long slab,
-                             hipStream_t st) {
-  // XT_M_WAB=0: LDS writes of the next K-tile before the barrier that closes this one
-  // (measured 1 % slower at the headline: 161.9-163.2 vs 159.8-160.9 ms/step)
-  const char* ewab = getenv("XT_M_WAB");      // read per call: tests switch it in-process
-  const int wab = ewab ? atoi(ewab) : 1;
-  if (wab)
-    hipLaunchKernelGGL((k_xc_back_m<TM, false, RV, NW, true>), dim3(blocks), dim3(64 * NW), 0, st, O, nx, V, n, kps,
-                       PO, ldp, W, wc, wg, R, rg, ws, (long)nx * V, slab);
-  else
-    hipLaunchKernelGGL((k_xc_back_m<TM, false, RV, NW>), dim3(blocks), dim3(64 * NW), 0, st, O, nx, V, n, kps, PO,
-                       ldp, W, wc, wg, R, rg, ws, (long)nx * V, slab);
-}
-
-// remainder rows on the VALU for the occupied counts of the BASELINE shapes
-// (O = 33..40: C2, C5; O = 97..104: the headline); XT_M_RV=0 keeps 16-row MFMA tiles
-template <int TM, int NW>
-static bool launch_back_m_valu(int O, int nx, int V, int n, int kps, int blocks, const double* PO, long ldp,
-                               const double* W, long wc, long wg, const double* R, long rg, double* ws, long slab,
-                               hipStream_t st) {
-  const int rv = O - 16 * (TM - 1);
-  if (TM == 7 && rv > 6) return false;                 // (spills at 256 VGPRs)
-#define XT_RV(N) case N: launch_back_m_rv<TM, N, NW>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); return true;
-  switch (rv) { XT_RV(1) XT_RV(2) XT_RV(3) XT_RV(4) XT_RV(5) XT_RV(6) XT_RV(7) XT_RV(8) default: return false; }
-#undef XT_RV
-}
-
-template <int TM, int NW>
+// remainder rows on the VALU for the occupied counts of the BASELINE shapes (O = 33..40:
+// C2, C5; O = 97..104: the headline): RV = O - 16 (TM - 1) <= 8 (<= 6 at TM 7: more
+// spills at 256 VGPRs); otherwise 16-row MFMA tiles throughout
+template <int TM>
 static void launch_back_m(int O, int nx, int V, int n, int kps, int blocks, const double* PO, long ldp,
                           const double* W, long wc, long wg, const double* R, long rg, double* ws, long slab,
                           hipStream_t st) {
-  const char* erv = getenv("XT_M_RV");
-  const int rv_on = erv ? atoi(erv) : 1;
+  const int rv = O - 16 * (TM - 1);
+  const dim3 grid(blocks), blk(64 * NW);
+  const long ldo = (long)nx * V;
   if constexpr (TM == 3 || TM == 7) {
-    if (rv_on && launch_back_m_valu<TM, NW>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st))
-      return;
+    if (!(TM == 7 && rv > 6)) {
+#define XT_RV(N) case N: hipLaunchKernelGGL((k_xc_back_m<TM, N>), grid, blk, 0, st, O, nx, V, n, kps, PO, ldp, W, wc, \
+                                            wg, R, rg, ws, ldo, slab); return;
+      switch (rv) { XT_RV(1) XT_RV(2) XT_RV(3) XT_RV(4) XT_RV(5) XT_RV(6) XT_RV(7) XT_RV(8) default: break; }
+#undef XT_RV
+    }
   }
-  const char* eg = getenv("XT_M_GEN");
-  if (eg && atoi(eg) == 1)
-    hipLaunchKernelGGL((k_xc_back_m<TM, true, 0, NW>), dim3(blocks), dim3(64 * NW), 0, st, O, nx, V, n, kps, PO,
-                       ldp, W, wc, wg, R, rg, ws, (long)nx * V, slab);
-  else
-    hipLaunchKernelGGL((k_xc_back_m<TM, false, 0, NW>), dim3(blocks), dim3(64 * NW), 0, st, O, nx, V, n, kps, PO,
-                       ldp, W, wc, wg, R, rg, ws, (long)nx * V, slab);
-}
-
-template <int NW>
-static void launch_back_m_tm(int TM, int O, int nx, int V, int n, int kps, int blocks, const double* PO, long ldp,
-                             const double* W, long wc, long wg, const double* R, long rg, double* ws, long slab,
-                             hipStream_t st) {
-#define XT_TM(N) case N: launch_back_m<N, NW>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
-  switch (TM) { XT_TM(1) XT_TM(2) XT_TM(3) XT_TM(4) XT_TM(5) XT_TM(6) XT_TM(7) default: XT_TM(8) }
-#undef XT_TM
+  hipLaunchKernelGGL((k_xc_back_m<TM>), grid, blk, 0, st, O, nx, V, n, kps, PO, ldp, W, wc, wg, R, rg, ws, ldo, slab);
 }
 
 int xc_back_m(int O, int nx, int V, int n, const double* PO, long ldp, const double* W, long wc, long wg,
@@ -433,10 +365,9 @@ int xc_back_m(int O, int nx, int V, int n, const double* PO, long ldp, const dou
   const long slab = (long)O * nx * V;
   if (ws_bytes < sizeof(double) * (size_t)p.splits * slab) return XT_ERR_ARG;
   const int TM = (O + 15) / 16;
-  if (p.nw == 4)
-    launch_back_m_tm<4>(TM, O, nx, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st);
-  else
-    launch_back_m_tm<8>(TM, O, nx, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st);
+#define XT_TM(N) case N: launch_back_m<N>(O, nx, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+  switch (TM) { XT_TM(1) XT_TM(2) XT_TM(3) XT_TM(4) XT_TM(5) XT_TM(6) XT_TM(7) default: XT_TM(8) }
+#undef XT_TM
   const long total = slab;
   int rb = (int)((total + 255) / 256);
   if (rb > 8192) rb = 8192;

@@ -5,16 +5,15 @@
 //
 // The intermediate T[g][xg][a] = sum_i PhiO Zp (nx V values per grid point) never
 // leaves registers.  MFMA orientation: rows = virtuals a, columns = grid points g,
-// K = occupied i.  A block covers 8 trial pairs and 16 TNG grid points; each of its
-// 8 / XW waves owns XW pairs (default TNG = 4, XW = 1: 64 points, 8 waves, one block
-// per CU; TNG = 2, XW = 2: 32 points, 4 waves, two blocks per CU):
+// K = occupied i.  A block covers 8 trial pairs and 64 grid points; each of its 8
+// waves owns one pair (one block per CU):
 //   * A = Zp[i][xg][a] (16 contiguous a per fragment row): loaded straight from
 //     global memory into registers through a 4-k-step ring (each wave's own pairs);
 //   * B = PhiO[g][i]: the block's 16 TNG x O tile, loaded ONCE per block into LDS
-//     and resident for the whole a loop; each B fragment feeds the wave's XW pairs;
+//     and resident for the whole a loop;
 //   * after each 32-wide a-tile's K loop the accumulators T[a][g] are contracted
-//     with dPhiV_c[g][a] (staged per a-tile in LDS, shared by the block's waves, each
-//     weight read feeding XW pairs) into per-lane partial sums racc[k][j][c] -- the
+//     with dPhiV_c[g][a] (staged per a-tile in LDS, shared by the block's waves)
+//     into per-lane partial sums racc[j][c] -- the
 //     sum over a stays in-lane (rows a of a lane are q + 4 reg + 16 t) and only the
 //     final 4-row reduction crosses lanes, once per block.
 // One barrier per a-tile (26 k-steps x 8 MFMAs per wave at O = 101).
@@ -24,7 +23,7 @@
 // the fragment / weight reads (16 consecutive g, two rows of opposite parity per
 // 32-lane group) land in opposite bank halves.
 #include <hip/hip_runtime.h>
-#include <stdlib.h>
+#include <mutex>
 #include <type_traits>
 #include "xt_internal.h"
 
@@ -36,10 +35,8 @@ typedef double d4w __attribute__((ext_vector_type(4)));
 constexpr int WA = 32;           // virtuals per a-tile (2 MFMA row sub-tiles)
 constexpr int TMA = WA / 16;
 constexpr int WXB = 8;           // trial pairs per block (one per wave)
-#ifndef XCW_ZD
-#define XCW_ZD 4
-#endif
-constexpr int ZD = XCW_ZD;       // Zp prefetch ring depth (k-steps)
+constexpr int ZD = 4;            // Zp prefetch ring depth (k-steps; 2 measured +6.5 %, 6 +2.8 %, 8 spills)
+constexpr int TNG = 4;           // 16-point column sub-tiles per block (64 grid points)
 
 __device__ __forceinline__ int swz(int row) { return (row & 15) | ((row & 1) << 4); }
 
@@ -56,26 +53,17 @@ __device__ __forceinline__ double rows4(double v) {
   return pair(pair(v, false), true);
 }
 
-// XW trial pairs per wave (WXB / XW waves per block, the block still covers WXB pairs):
-// XW = 2 runs one wave per SIMD with twice the accumulators (the MFMA accumulators in
-// AGPRs), each B fragment and weight read feeding both pairs.
-template <int TNG, bool BRANCHY, int XW = 1, int ZDT = XCW_ZD>
-__global__ void __launch_bounds__(64 * WXB / XW)
-__attribute__((amdgpu_waves_per_eu(XW == 2 ? (TNG <= 2 ? 2 : 1) : (TNG <= 2 ? 4 : 2), XW == 2 ? (TNG <= 2 ? 2 : 1) : (TNG <= 2 ? 4 : 2))))
+__global__ void __launch_bounds__(64 * WXB) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_xc_rho_w(int O, int nx, int V, int n,
            const double* __restrict__ PO, long ldp,
            const double* __restrict__ Z, long zi, long zx,
            const double* __restrict__ Wg, long wc, long wg,
-           double* __restrict__ Rout, long rg, int xs_fast) {
+           double* __restrict__ Rout, long rg) {
   constexpr int GB = 16 * TNG;                 // grid points per block
-  constexpr int ZD = ZDT;                      // Zp ring depth (k-steps)
   constexpr int W_IMG = 3 * WA * GB;           // one weight buffer (doubles)
-  constexpr int NT = 64 * WXB / XW;            // threads per block
-  // XW = 2 stages each a-tile's weights in two halves (loaded before / stored after
-  // each half of the K loop) to halve the staging registers
-  constexpr int WPH = (XW == 2 && TNG == 4) ? 2 : 1;   // staging phases per a-tile
-  constexpr int W_LD = W_IMG / NT / WPH;       // weight elements staged per thread and phase
-  static_assert(W_IMG % (NT * WPH) == 0, "weight staging map");
+  constexpr int NT = 64 * WXB;                 // threads per block
+  constexpr int W_LD = W_IMG / NT;             // weight elements staged per thread
+  static_assert(W_IMG % NT == 0, "weight staging map");
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int KI = (O + 7) & ~7;                 // occupied rows in the image (k-steps even)
   double* sP = sm;                             // [KI][GB]
@@ -94,20 +82,12 @@ k_xc_rho_w(int O, int nx, int V, int n,
     const int xcd = lid & 7, idx = lid >> 3, qn = nblk >> 3, rem = nblk & 7;
     lid = xcd * qn + (xcd < rem ? xcd : rem) + idx;
   }
-  // xs_fast (XT_W_ORDER=1): the trial-pair sets of one g-tile side by side instead (they
-  // share the g-tile's gradient weights in L2; the Zp slices then come from MALL)
-  const int nxs = (nx + WXB - 1) / WXB;
-  const int gt = xs_fast ? lid / nxs : lid % ntg, xs = xs_fast ? lid % nxs : lid / ntg;
+  // (trial-pair sets of one g-tile side by side instead, sharing its gradient weights
+  // in L2: neutral, 168.1-168.3 vs 168.2-168.6 ms/step)
+  const int gt = lid % ntg, xs = lid / ntg;
   const int g0 = gt * GB, x0 = xs * WXB;
-  const int xg = x0 + wave * XW;               // this wave's first trial pair
+  const int xg = x0 + wave;                    // this wave's trial pair
   const bool wave_on = xg < nx;
-  long koff[XW];                               // Zp offset of pair k (pairs past nx: pair xg again)
-  bool kon[XW];
-#pragma unroll
-  for (int k = 0; k < XW; ++k) {
-    kon[k] = xg + k < nx;
-    koff[k] = kon[k] ? (long)k * zx : 0L;
-  }
   const int nat = (V + WA - 1) / WA;
   const int KS = KI / 4;
 
@@ -119,68 +99,50 @@ k_xc_rho_w(int O, int nx, int V, int n,
   }
   // ---- weights of a-tile `at` (global -> registers -> LDS) -------------------
   double rw[W_LD];
-  auto load_w = [&](int at, int ph = 0) XT_INLINE {
+  auto load_w = [&](int at) XT_INLINE {
 #pragma unroll
     for (int e = 0; e < W_LD; ++e) {
-      const int p = tid + NT * (e + ph * W_LD), c = p / (WA * GB), g = (p / WA) % GB, a = p % WA;
+      const int p = tid + NT * e, c = p / (WA * GB), g = (p / WA) % GB, a = p % WA;
       rw[e] = Wg[c * wc + (long)(g0 + g) * wg + min(at * WA + a, V - 1)];
     }
   };
-  auto store_w = [&](int buf, int at, int ph = 0) XT_INLINE {
+  auto store_w = [&](int buf, int at) XT_INLINE {
 #pragma unroll
     for (int e = 0; e < W_LD; ++e) {
-      const int p = tid + NT * (e + ph * W_LD), c = p / (WA * GB), g = (p / WA) % GB, a = p % WA;
+      const int p = tid + NT * e, c = p / (WA * GB), g = (p / WA) % GB, a = p % WA;
       sW[buf * W_IMG + (c * WA + a) * GB + (g ^ swz(a))] = at * WA + a < V ? rw[e] : 0.0;
     }
   };
-#pragma unroll
-  for (int ph = 0; ph < WPH; ++ph) {
-    load_w(0, ph);
-    store_w(0, 0, ph);
-  }
+  load_w(0);
+  store_w(0, 0);
 
   // ---- Zp ring: k-step u of the whole a loop (a-tile u / KS, k-step u % KS) ----
   // lane (q, r16) loads rows i = 4 s + q (past O: zeroed slack rows of Zp) of
   // columns at WA + 16 t + r16 (past V: the next pair's values, weighted by zero)
   const double* zb = Z + (long)(wave_on ? xg : 0) * zx + r16 + (long)q * zi;
-  double zq[ZD][XW][TMA];
+  double zq[ZD][TMA];
   const long zstep = 4 * zi;
   const double* zn = zb;                       // next k-step to load: a-tile za, k-step zs
   int zs = 0, za = 0;
   // advance to the next k-step; past the a-tile's last k-step the pointer jumps to the
   // next tile's first row (the last tile repeats itself: those loads are never
-  // consumed).  BRANCHY (default): an if/else, which splits the unrolled K loop into
-  // one basic block per k-step; the select-based form keeps one block per 4 k-steps
-  // but measured 4 % slower.
-  const long zwrap = (long)WA - (long)KS * zstep;
+  // consumed).  An if/else, which splits the unrolled K loop into one basic block per
+  // k-step (a select-based form with one block per 4 k-steps measured 4 % slower).
   auto load_z = [&](int slot) XT_INLINE {
 #pragma unroll
-    for (int k = 0; k < XW; ++k)
-#pragma unroll
-      for (int t = 0; t < TMA; ++t) zq[slot][k][t] = zn[koff[k] + 16 * t];
-    if constexpr (BRANCHY) {
-      if (++zs == KS) { zs = 0; za = za + 1 < nat ? za + 1 : za; zn = zb + za * WA; }
-      else zn += zstep;
-    } else {
-      ++zs;
-      const bool wrap = zs == KS;
-      const bool last = za + 1 >= nat;
-      zs = wrap ? 0 : zs;
-      za = wrap ? za + 1 : za;
-      zn += zstep + (wrap ? (last ? -(long)KS * zstep : zwrap) : 0L);
-    }
+    for (int t = 0; t < TMA; ++t) zq[slot][t] = zn[16 * t];
+    if (++zs == KS) { zs = 0; za = za + 1 < nat ? za + 1 : za; zn = zb + za * WA; }
+    else zn += zstep;
   };
 #pragma unroll
   for (int d = 0; d < ZD; ++d) load_z(d);
 
-  d4w acc[XW][TMA][TNG];
-  double racc[XW][TNG][3];
+  d4w acc[TMA][TNG];
+  double racc[TNG][3];
 #pragma unroll
-  for (int k = 0; k < XW; ++k)
+  for (int j = 0; j < TNG; ++j)
 #pragma unroll
-    for (int j = 0; j < TNG; ++j)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) racc[k][j][c] = 0.0;
+    for (int c = 0; c < 3; ++c) racc[j][c] = 0.0;
 
   const int p_lane = q * GB;                   // B image: row 4 s + q, column (16 j + r16) ^ swz
   // one k-step from ring slot `slot` (a compile-time constant after unrolling)
@@ -190,19 +152,15 @@ k_xc_rho_w(int O, int nx, int V, int n,
     double bf[TNG];
 #pragma unroll
     for (int j = 0; j < TNG; ++j) bf[j] = sP[p_lane + 4 * s * GB + ((16 * j + r16) ^ sw)];
-    double af[XW][TMA];
+    double af[TMA];
 #pragma unroll
-    for (int k = 0; k < XW; ++k)
-#pragma unroll
-      for (int t = 0; t < TMA; ++t) af[k][t] = zq[slot][k][t];
+    for (int t = 0; t < TMA; ++t) af[t] = zq[slot][t];
     load_z(slot);
 #pragma unroll
-    for (int k = 0; k < XW; ++k)
+    for (int t = 0; t < TMA; ++t)
 #pragma unroll
-      for (int t = 0; t < TMA; ++t)
-#pragma unroll
-        for (int j = 0; j < TNG; ++j)
-          acc[k][t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[k][t], bf[j], acc[k][t][j], 0, 0, 0);
+      for (int j = 0; j < TNG; ++j)
+        acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t], bf[j], acc[t][j], 0, 0, 0);
   };
   // the K loop of one a-tile whose first k-step sits in ring slot PH (KS is even, so
   // PH is even); the slots stay compile-time constants inside each unrolled group
@@ -219,40 +177,21 @@ k_xc_rho_w(int O, int nx, int V, int n,
   };
   // k-steps [s0, s1) of a-tile at (s0 even: the ring phase stays even)
   auto krange = [&](int at, int s0, int s1) XT_INLINE {
+    static_assert(ZD == 4, "ring phases");
     const int ph = (int)(((long)at * KS + s0) % ZD);
-    if constexpr (ZD == 4) {
-      if (ph == 0) kloop(std::integral_constant<int, 0>{}, s0, s1);
-      else         kloop(std::integral_constant<int, 2>{}, s0, s1);
-    } else {
-      switch (ph) {
-        case 0: kloop(std::integral_constant<int, 0>{}, s0, s1); break;
-        case 2: kloop(std::integral_constant<int, 2 % ZD>{}, s0, s1); break;
-        case 4: kloop(std::integral_constant<int, 4 % ZD>{}, s0, s1); break;
-        default: kloop(std::integral_constant<int, 6 % ZD>{}, s0, s1); break;
-      }
-    }
+    if (ph == 0) kloop(std::integral_constant<int, 0>{}, s0, s1);
+    else         kloop(std::integral_constant<int, 2>{}, s0, s1);
   };
-  const int khalf = WPH == 2 ? ((KS / 2) & ~1) : KS;
   __syncthreads();
   for (int at = 0; at < nat; ++at) {
     const int buf = at & 1;
-    if (at + 1 < nat) load_w(at + 1, 0);
+    if (at + 1 < nat) load_w(at + 1);
 #pragma unroll
-    for (int k = 0; k < XW; ++k)
+    for (int t = 0; t < TMA; ++t)
 #pragma unroll
-      for (int t = 0; t < TMA; ++t)
-#pragma unroll
-        for (int j = 0; j < TNG; ++j) acc[k][t][j] = (d4w){0.0, 0.0, 0.0, 0.0};
-    if constexpr (WPH == 2) {
-      if (wave_on) krange(at, 0, khalf);
-      __builtin_amdgcn_sched_barrier(0);
-      if (at + 1 < nat) {
-        store_w(buf ^ 1, at + 1, 0);
-        load_w(at + 1, 1);
-      }
-    }
+      for (int j = 0; j < TNG; ++j) acc[t][j] = (d4w){0.0, 0.0, 0.0, 0.0};
     if (wave_on) {
-      krange(at, WPH == 2 ? khalf : 0, KS);
+      krange(at, 0, KS);
       // contraction with the a-tile's weights: acc[t][j][r] = T[a = 16 t + q + 4 r][g = 16 j + r16].
       // Half a row (t, r) of weights at a time, the next half's reads issued before this
       // half's FMAs (two 6-value buffers; unfenced, the compiler hoists all 96 reads and
@@ -279,104 +218,61 @@ k_xc_rho_w(int O, int nx, int V, int n,
         const int rw = h / 2, j0 = (h % 2) * JH;
         const int t = rw / 4, r = rw % 4;
 #pragma unroll
-        for (int k = 0; k < XW; ++k)
+        for (int jj = 0; jj < JH; ++jj)
 #pragma unroll
-          for (int jj = 0; jj < JH; ++jj)
-#pragma unroll
-            for (int c = 0; c < 3; ++c)
-              racc[k][j0 + jj][c] += acc[k][t][j0 + jj][r] * wb[h & 1][3 * jj + c];
+          for (int c = 0; c < 3; ++c)
+            racc[j0 + jj][c] += acc[t][j0 + jj][r] * wb[h & 1][3 * jj + c];
         __builtin_amdgcn_sched_barrier(0);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (at + 1 < nat) store_w(buf ^ 1, at + 1, WPH - 1);
+    if (at + 1 < nat) store_w(buf ^ 1, at + 1);
     __syncthreads();
   }
   if (!wave_on) return;
 #pragma unroll
-  for (int k = 0; k < XW; ++k)
+  for (int j = 0; j < TNG; ++j) {
+    const int g = g0 + 16 * j + r16;
 #pragma unroll
-    for (int j = 0; j < TNG; ++j) {
-      const int g = g0 + 16 * j + r16;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const double v = rows4(racc[k][j][c]);
-        if (kon[k] && q == 0 && g < n) Rout[(long)g * rg + 3 * (xg + k) + c] = v;
-      }
+    for (int c = 0; c < 3; ++c) {
+      const double v = rows4(racc[j][c]);
+      if (q == 0 && g < n) Rout[(long)g * rg + 3 * xg + c] = v;
     }
+  }
 }
 
-// Default: 64-point blocks of 8 one-pair waves.  XT_W_TNG=2 XT_W_XW=2: 32-point blocks
-// of 4 two-pair waves, two blocks per CU (each B fragment and weight read feeds two
-// pairs; the two independent blocks de-phase their barriers and contractions):
-// 163.3-163.5 vs 168.2-168.8 ms/step on one box, 169.8-170.1 vs 168.9 on another --
-// not a reproducible gain, so not the default.  XT_W_TNG=2 alone: 178 ms/step; TNG 4
-// with two pairs per wave spills (345 ms/step).
-static int w_tng() {
-  const char* e = getenv("XT_W_TNG");          // read per call: tests switch it in-process
-  return e && atoi(e) == 2 ? 2 : 4;
-}
-
-static int w_order() {                         // XT_W_ORDER=1: trial-pair sets fastest
-  const char* e = getenv("XT_W_ORDER");
-  return e && atoi(e) == 1 ? 1 : 0;
-}
-
-static int w_xw() {
-  const char* e = getenv("XT_W_XW");
-  return e && atoi(e) == 2 ? 2 : 1;
-}
-
-static size_t rho_w_lds(int O, int tng) {
-  const int GB = 16 * tng;
+// Measured and removed: 32-point blocks, two per CU (178 vs 168 ms/step);
+// two trial pairs per wave on 32-point blocks (163.3 vs 168.5 on one box, 170.0 vs 168.9
+// on another: not reproducible); two pairs per wave on 64-point blocks (spills, 345).
+static size_t rho_w_lds(int O) {
+  constexpr int GB = 16 * TNG;
   return sizeof(double) * ((size_t)((O + 7) & ~7) * GB + 2 * 3 * WA * GB);
 }
 
-size_t xc_rho_w_lds_bytes(int O) { return rho_w_lds(O, w_tng()); }
+size_t xc_rho_w_lds_bytes(int O) { return rho_w_lds(O); }
 
-template <int TNG, int XW = 1, int ZDT = XCW_ZD>
-static void launch_rho_w(int branchy, int blocks, size_t lds, hipStream_t st, int O, int nx, int V, int n,
-                         const double* PO, long ldp, const double* Z, long zi, long zx, const double* W, long wc,
-                         long wg, double* R, long rg) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_xc_rho_w<TNG, false, XW, ZDT>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_xc_rho_w<TNG, true, XW, ZDT>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
-  const int nt = 64 * WXB / XW;
-  if (branchy)
-    hipLaunchKernelGGL((k_xc_rho_w<TNG, true, XW, ZDT>), dim3(blocks), dim3(nt), lds, st, O, nx, V, n, PO, ldp, Z,
-                       zi, zx, W, wc, wg, R, rg, w_order());
-  else
-    hipLaunchKernelGGL((k_xc_rho_w<TNG, false, XW, ZDT>), dim3(blocks), dim3(nt), lds, st, O, nx, V, n, PO, ldp, Z,
-                       zi, zx, W, wc, wg, R, rg, w_order());
+// the 160 KB dynamic-LDS attribute, set once per device (thread-safe)
+static void rho_w_lds_attribute() {
+  static std::mutex mu;
+  static unsigned long long done = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  if (dev < 64 && (done >> dev & 1ull)) return;
+  (void)hipFuncSetAttribute((const void*)k_xc_rho_w, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (dev < 64) done |= 1ull << dev;
 }
 
 int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const double* Z, long zi, long zx,
              const double* W, long wc, long wg, double* R, long rg, hipStream_t st) {
   if (O <= 0 || nx <= 0 || V <= 0 || n <= 0) return 0;
-  const int tng = w_tng();
-  const size_t lds = rho_w_lds(O, tng);
+  const size_t lds = rho_w_lds(O);
   if (lds > 160 * 1024) return XT_ERR_ARG;
-  // XT_W_RING=0: the select-based (branch-free) ring advance; measured slower on the
-  // same box (178.2 vs 170.6 ms/step; engine mode 1: 173.4)
-  const char* ering = getenv("XT_W_RING");    // read per call: tests switch it in-process
-  const int branchy = ering ? atoi(ering) : 1;
-  const int GB = 16 * tng;
+  rho_w_lds_attribute();
+  constexpr int GB = 16 * TNG;
   const int blocks = ((n + GB - 1) / GB) * ((nx + WXB - 1) / WXB);
-  if (tng == 2 && w_xw() == 2)
-    launch_rho_w<2, 2>(branchy, blocks, lds, st, O, nx, V, n, PO, ldp, Z, zi, zx, W, wc, wg, R, rg);
-  else if (tng == 2)
-    launch_rho_w<2>(branchy, blocks, lds, st, O, nx, V, n, PO, ldp, Z, zi, zx, W, wc, wg, R, rg);
-  else if (w_xw() == 2)
-    launch_rho_w<4, 2>(branchy, blocks, lds, st, O, nx, V, n, PO, ldp, Z, zi, zx, W, wc, wg, R, rg);
-  else if (getenv("XT_W_ZD") && atoi(getenv("XT_W_ZD")) == 6)   // a 6-k-step Zp ring
-    launch_rho_w<4, 1, 6>(branchy, blocks, lds, st, O, nx, V, n, PO, ldp, Z, zi, zx, W, wc, wg, R, rg);
-  else
-    launch_rho_w<4>(branchy, blocks, lds, st, O, nx, V, n, PO, ldp, Z, zi, zx, W, wc, wg, R, rg);
+  hipLaunchKernelGGL(k_xc_rho_w, dim3(blocks), dim3(64 * WXB), lds, st, O, nx, V, n, PO, ldp, Z, zi, zx, W, wc, wg,
+                     R, rg);
   return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
 }
 

@@ -33,8 +33,8 @@ def allreduce_sigma(sigma, group=None):
 
     A torch tensor is reduced in place (through a host copy when the backend
     is gloo and the tensor lives on the GPU, through a device copy when the
-    backend is RCCL and it lives on the host); a NumPy array is reduced the
-    same way and returned as a new array."""
+    backend is RCCL and it lives on the host); a NumPy array is left untouched
+    and the sum is returned as a new array."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -42,7 +42,7 @@ def allreduce_sigma(sigma, group=None):
         return sigma
     nccl = dist.get_backend(group) == "nccl"
     if isinstance(sigma, np.ndarray):
-        t = torch.from_numpy(np.ascontiguousarray(sigma, dtype=np.float64))
+        t = torch.tensor(np.asarray(sigma, dtype=np.float64))      # a copy: the input stays as it was
         if nccl:     # RCCL reduces device tensors only
             d = t.to(f"cuda:{torch.cuda.current_device()}")
             dist.all_reduce(d, group=group)
