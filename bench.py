@@ -278,6 +278,34 @@ def _time_call(f, reps, what=""):
     return float(np.median(ts))
 
 
+class _CyclicGrid:
+    """Full-size grid data for the oracle, streamed: the oracle walks the grid in
+    blocks of oracle.engines.GRID_BLOCK points (ao[:ncomp, g0:g1], weights[g0:g1],
+    fxc[..., g0:g1]); block b is served from stored block b mod nb.  The BLAS work
+    per block depends on the shape, not the values, so the timing is that of the
+    full grid without its 38 GB of AO values in host memory."""
+
+    class _View:
+        def __init__(self, blocks, axis_last, ngrid, gb):
+            self.blocks, self.ngrid, self.gb = blocks, ngrid, gb
+
+        def __getitem__(self, key):
+            key = key if isinstance(key, tuple) else (key,)
+            sl = key[-1]
+            g0, g1 = sl.start or 0, self.ngrid if sl.stop is None else min(sl.stop, self.ngrid)
+            b = self.blocks[(g0 // self.gb) % len(self.blocks)]
+            return b[key[:-1] + (slice(0, g1 - g0),)]
+
+    def __init__(self, ao_blocks, w_blocks, ngrid, gb):
+        self.ao = self._View(ao_blocks, True, ngrid, gb)
+        self.weights = self._View(w_blocks, True, ngrid, gb)
+        self._ngrid = ngrid
+
+    @property
+    def ngrid(self):
+        return self._ngrid
+
+
 def cpu_baseline(args):
     """The oracle's A.x (the reference's AO-route algorithm, NumPy/BLAS) on ALL
     host cores, one trial vector per call.
@@ -285,17 +313,15 @@ def cpu_baseline(args):
     Threads: every CPU this process may run on (``cpu_share``: the host's CPUs
     capped by the cgroup quota of a shared GPU box; more BLAS threads than the
     quota only oversubscribe it).  Shapes whose AO grid data stay small are timed
-    at the full (naux, ngrid), 1 warm-up + median of 5.  The large ones:
-    t = t_A + s (ngrid - g1) with t_A timed at the FULL naux and ngrid g1 (one
-    call of tens of seconds, after a warm-up of the same vind at a small naux)
-    and the grid slope s from two grid sizes at a small naux (1 warm-up +
-    median of 5 each; the J/K work does not depend on the grid and the blockwise
-    grid loop is linear in ngrid), so only the grid dimension is extrapolated.
-    The exact-K configuration contracts stored 4-index ERIs (the incore
-    mf._eri route), built from the same factor.  Returns matvecs/s."""
+    at the full (naux, ngrid), 1 warm-up + median of 5.  The large ones are timed
+    as ONE call at the full naux and the full ngrid (after a warm-up call of the
+    same vind at a small size): the DF factor is a small factor tiled to naux and
+    the grid is streamed block by block from a few stored blocks (``_CyclicGrid``),
+    so nothing is extrapolated.  The exact-K configuration contracts stored 4-index
+    ERIs (the incore mf._eri route), built from the same factor.  Returns matvecs/s."""
     import dataclasses
     from threadpoolctl import threadpool_info, threadpool_limits
-    from oracle.engines import eri_full_from_cderi
+    from oracle.engines import GRID_BLOCK, eri_full_from_cderi
     from xtddft_amd.synthetic import make_mf, make_trial_vectors
     ncpu = cpu_share()
     t_all = time.perf_counter()
@@ -321,29 +347,33 @@ def cpu_baseline(args):
             t = t_vec(build(args.naux, args.ngrid), 5, "full size")
             how = f"timed at the full size (naux={args.naux}, ngrid={args.ngrid}), 1 warm-up + median of 5"
         else:
-            g1, g2, n_small = 8192, 24576, 16
-            small = build(n_small, g1)
+            n_small, nblk = 16, 2
+            small = build(n_small, nblk * GRID_BLOCK)
             # full-naux factor: the small factor tiled (the BLAS work depends on the
             # shape, not the values; avoids generating 8 naux nao^2 bytes of normals)
             reps_ = -(-args.naux // n_small)
+            ao, w = small.grids.ao, small.grids.weights
+            blocks = [slice(b * GRID_BLOCK, (b + 1) * GRID_BLOCK) for b in range(nblk)]
+            grid = _CyclicGrid([ao[:, b] for b in blocks], [w[b] for b in blocks], args.ngrid, GRID_BLOCK)
+            fxc = _CyclicGrid._View([small.fxc[..., b] for b in blocks], True, args.ngrid, GRID_BLOCK)
+            fsf = _CyclicGrid._View([small.fxc_sf[b] for b in blocks], True, args.ngrid, GRID_BLOCK)
             big = dataclasses.replace(small, cderi=np.tile(small.cderi, (reps_, 1, 1))[:args.naux]
-                                      * np.sqrt(n_small / args.naux))
+                                      * np.sqrt(n_small / args.naux), grids=grid, fxc=fxc, fxc_sf=fsf)
             vind_s, hd = _oracle_vind(args, small)
+            t0 = time.perf_counter()
             vind_s(make_trial_vectors(1, hd.size))          # warms BLAS threads and allocators
+            log(f"cpu baseline warm-up (naux={n_small}, ngrid={nblk * GRID_BLOCK}): "
+                f"{time.perf_counter() - t0:.2f} s")
             vind_b, _ = _oracle_vind(args, big)
             z1 = make_trial_vectors(1, hd.size)
+            log(f"cpu baseline: one call at naux={args.naux}, ngrid={args.ngrid} (streamed grid)")
             t0 = time.perf_counter()
             vind_b(z1)
-            t_a = time.perf_counter() - t0
-            log(f"cpu baseline naux={args.naux} ngrid={g1}: {t_a:.2f} s")
-            del big, vind_b
-            s1 = t_vec(small, 5, f"naux={n_small} ngrid={g1}")
-            s2 = t_vec(build(n_small, g2), 5, f"naux={n_small} ngrid={g2}")
-            slope = (s2 - s1) / (g2 - g1)
-            t = t_a + slope * (args.ngrid - g1)
-            how = (f"timed at the full naux={args.naux} with ngrid={g1} ({t_a:.2f} s, one call) plus the grid slope {slope * 1e6:.3f} s per 1e6 points from ngrid {g1} / {g2} "
-                   f"at naux={n_small} ({s1:.3f} / {s2:.3f} s, 1 warm-up + median of 5); "
-                   f"extrapolated in ngrid only, to {args.ngrid}")
+            t = time.perf_counter() - t0
+            log(f"cpu baseline naux={args.naux} ngrid={args.ngrid}: {t:.2f} s")
+            how = (f"one call timed at the full naux={args.naux} and the full ngrid={args.ngrid} (grid streamed "
+                   f"in {GRID_BLOCK}-point blocks cycling {nblk} stored blocks, the DF factor tiled from "
+                   f"{n_small} functions), after a warm-up call at naux={n_small}, ngrid={nblk * GRID_BLOCK}")
     return dict(value=1.0 / t, unit="matvecs/s", cores=int(threads), kind="port",
                 sample=(f"oracle {KIND_NAME[args.kind]} vind (NumPy AO route, "
                         f"{'stored 4-index ERI' if args.jk == 'ERI8' else 'DF'} J/K, {args.xc}) on 1 vector "
@@ -456,12 +486,40 @@ def roofline_of(args, stats_acc, steps, world=1):
                     frac=round(gbs / HBM_PEAK_GBS, 4), traffic=traffic, kernel=dom_name,
                     avg_launch_ms=round(avg_ms, 4), bytes_per_launch=bytes_launch,
                     launches_per_step=dom["launches"] / steps)
-    flops_launch = dom["flops"] / max(1, dom["launches"])
+    flops_fused = dom["flops"] / max(1, dom["launches"])
+    # algorithmic flops: 2 G nvec sum_s o_s v_s per XC class -- the
+    # library counts the superset block (O x V per channel) and, for the two fused
+    # classes, their gradient contraction / operand generation (2 (O + 3) per element)
+    flops_launch = flops_fused * strict_factor(args, dom_name)
     achieved = flops_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+    fused = flops_fused / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     return dict(bound="mfma", achieved=round(achieved, 3), peak=FP64_PEAK_TFLOPS, unit="TFLOP/s",
                 frac=round(achieved / FP64_PEAK_TFLOPS, 4), traffic=traffic,
                 kernel=dom_name, avg_launch_ms=round(avg_ms, 4),
-                flops_per_launch=flops_launch, launches_per_step=dom["launches"] / steps)
+                flops_per_launch=flops_launch, launches_per_step=dom["launches"] / steps,
+                accounting="strict: 2 G nvec sum_s o_s v_s (SURVEY.md 8(d))",
+                achieved_fused_accounting=round(fused, 3),
+                frac_fused_accounting=round(fused / FP64_PEAK_TFLOPS, 4))
+
+
+def strict_factor(args, name):
+    """Algorithmic / counted flops of an XC class: the actual occupied-virtual pairs
+    over the superset block the kernels run (both X-TDA channels as O x V), times
+    O / (O + 3) for the fused classes (their 3-FMA contraction / generation counted by
+    the library as extra rows)."""
+    if name not in ("xc_forward_u", "xc_back_l", "xc_forward_w", "xc_back_m"):
+        return 1.0
+    if args.kind == "XTDA":
+        O, V = args.nc + args.no, args.no + args.nv
+        pairs, sup = (args.nc + args.no) * args.nv + args.nc * (args.no + args.nv), 2 * O * V
+    elif args.kind == "SF_UP":
+        O = args.nc
+        pairs = sup = args.nc * args.nv
+    else:
+        O = args.nc + args.no
+        pairs = sup = O * (args.no + args.nv)
+    f = pairs / sup
+    return f * O / (O + 3) if name in ("xc_forward_w", "xc_back_m") else f
 
 
 def breakdown(op, z, out, allreduce, sync, stats_acc, steps, rank, world, reps=2):
@@ -566,7 +624,8 @@ def rank_main(args):
         comp = v["bytes"] / v["launches"]
         hbm = None if (args.custom or world > 1) else load_traffic(args.config, k)
         others[k] = dict(ms_per_step=round(v["ms"] / args.steps, 3),
-                         tflops=round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 3),
+                         tflops=round(v["flops"] * strict_factor(args, k) / max(v["ms"], 1e-9) / 1e9, 3),
+                         tflops_fused_accounting=round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 3),
                          compulsory_bytes_per_launch=comp, hbm_bytes_per_launch=hbm,
                          traffic_ratio=round(hbm / comp, 3) if hbm and comp > 0 else None)
     workload = (f"{KIND_NAME[args.kind]} A.x, nao={args.nao}, nocc_a/nocc_b={args.nc + args.no}/{args.nc}, "

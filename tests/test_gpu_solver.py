@@ -126,3 +126,85 @@ def test_davidson_follow_state_and_lessio_accepted(torch):
     c1, e1, _, _ = davidson1(op.apply, x0, DiagPrecond(hdiag, 0.0), **kw)
     c2, e2, _, _ = davidson1(op.apply, x0, DiagPrecond(hdiag, 0.0), follow_state=True, lessio=True, **kw)
     assert c1.all() and c2.all() and np.abs(np.asarray(e1) - np.asarray(e2)).max() < 1e-10
+
+
+def _mgs_host(x, lindep):
+    """PySCF _qr on the host (modified Gram-Schmidt, drop norm**2 <= lindep)."""
+    q = []
+    for row in x:
+        v = row.copy()
+        for u in q:
+            v -= u * (u @ v)
+        for u in q:
+            v -= u * (u @ v)
+        n2 = v @ v
+        if n2 > lindep:
+            q.append(v / np.sqrt(n2))
+    return np.asarray(q)
+
+
+@pytest.mark.parametrize("eps", [1e-3, 1e-5, 1e-6])
+def test_qr_near_collinear_rows(torch, eps):
+    """Blocks with nearly collinear rows at lindep 1e-14 (the SF drivers' value,
+    SF_TDA.py:392): the block QR keeps the same rows as the vector-by-vector
+    reference rule and its output is orthonormal to round-off (the
+    Gram-matrix route squares the conditioning; nearly dependent blocks take the
+    vector-wise path)."""
+    from xtddft_amd.davidson import _Dev, _qr, _qr_vectorwise
+    rng = np.random.default_rng(11)
+    dim = 600
+    base = rng.normal(size=(5, dim))
+    rows = [base[0], base[1], base[0] + eps * rng.normal(size=dim), base[2],
+            base[1] + eps * rng.normal(size=dim), 0.5 * base[0] + 2 * base[2],      # exactly dependent
+            base[3], base[2] + eps * rng.normal(size=dim), base[4]]
+    x = np.asarray(rows)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    dev = _Dev(0)
+    xt = torch.as_tensor(x, device="cuda")
+    q = _qr(dev, xt, 1e-14).cpu().numpy()
+    qv = _qr_vectorwise(dev, xt, 1e-14).cpu().numpy()
+    ref = _mgs_host(x, 1e-14)
+    assert q.shape[0] == qv.shape[0] == ref.shape[0] == 8
+    for a in (q, qv):
+        assert np.abs(a @ a.T - np.eye(a.shape[0])).max() < 1e-12
+        # same span as the reference
+        assert np.abs(a @ ref.T @ ref - a).max() < 1e-9
+
+
+def test_davidson_follow_state_restart_branch(torch):
+    """An aop that corrupts one step's images (a residual blow-up) makes follow_state restart
+    from the previous Ritz vectors (Davidson.py:246-253): the next block lies in the
+    span of the subspace before the corrupted step, and the solver still converges
+    to the uncorrupted roots."""
+    from xtddft_amd.davidson import DiagPrecond, davidson1
+    from xtddft_amd.operator import DeviceOperator
+    mf = make_mf(nao=30, nc=6, no=2, xctype="GGA", hyb=0.2)
+    vind, hdiag = oxtda.gen_tda_operation(mf)
+    x0 = oxtda.get_init_guess(mf, 3)
+    op = DeviceOperator(mf, "XTDA")
+    w = np.linalg.eigvalsh(vind(np.eye(hdiag.size)).T)
+    blocks, state = [], dict(calls=0, hit=None)
+
+    def aop(xt):
+        blocks.append(xt.cpu().numpy().copy())
+        s = op.apply(xt)
+        state["calls"] += 1
+        if state["calls"] == 4:
+            # add a direction outside the subspace to every image: the subspace matrix is
+            # unchanged, the residuals of this step blow up
+            state["hit"] = len(blocks) - 1
+            span, _ = np.linalg.qr(np.concatenate(blocks).T)
+            u = np.random.default_rng(5).normal(size=span.shape[0])
+            u -= span @ (span.T @ u)
+            u /= np.linalg.norm(u)
+            s = s + 200.0 * torch.as_tensor(np.broadcast_to(u, s.shape).copy(), device=s.device)
+        return s
+    c, e, _, _ = davidson1(aop, x0, DiagPrecond(hdiag, 0.0), tol_residual=1e-6, lindep=1e-12, nroots=3,
+                           pick=oxtda.pickeig, max_cycle=100, follow_state=True, max_space=30)
+    k = state["hit"]
+    assert k is not None and len(blocks) > k + 1
+    before = np.concatenate(blocks[:k])
+    qb, _ = np.linalg.qr(before.T)
+    nxt = blocks[k + 1]
+    assert np.abs(nxt.T - qb @ (qb.T @ nxt.T)).max() < 1e-8      # restarted inside the old span
+    assert c.all() and np.abs(np.asarray(e) - w[:3]).max() < 1e-8

@@ -105,3 +105,32 @@ def test_stored_exchange_small_row_counts(hiplib, kind, nz):
     z = make_trial_vectors(nz, hdiag.size)
     op = DeviceOperator(mf, kind, k_mode="stored")
     assert rel(op.apply(z), vind(z)) < RTOL
+
+
+@pytest.mark.parametrize("nz", [1, 2, 3, 5, 7, 13])
+@pytest.mark.parametrize("nc,no,nao", [(5, 2, 26), (33, 1, 60), (95, 2, 130), (99, 2, 140), (120, 3, 150)])
+@pytest.mark.parametrize("knobs", [dict(), dict(XT_W_KERNEL=1)])
+def test_xc_kernels_small_batches(hiplib, env, knobs, nz, nc, no, nao):
+    """Davidson steps with few new vectors: nx = 2 nz = 2, 4, 6, 10, 14, 26 trial pairs
+    take the dedicated kernels' small-batch shapes (rho-forward: 8, 4, 2 or 1 pairs per
+    block with a pair's k-steps split over 8 / PB waves; M-backward: blocks of 8, 4, 2 or
+    1 waves) -- against the oracle."""
+    from xtddft_amd.operator import DeviceOperator
+    env(**knobs)
+    mf = make_mf(nao=nao, nc=nc, no=no, ngrid=3000, xctype="GGA", hyb=0.2)
+    vind, hdiag = oxtda.gen_tda_operation(mf)
+    z = make_trial_vectors(nz, hdiag.size)
+    op = DeviceOperator(mf, "XTDA")
+    assert rel(op.apply(z), vind(z)) < RTOL
+
+
+@pytest.mark.parametrize("nz", [1, 3, 30])
+def test_sf_up_single_channel_small_batches(hiplib, nz):
+    """SF-up (one channel: nx = nz, odd counts) through the same small-batch shapes."""
+    from oracle import sf_tda as osf
+    from xtddft_amd.operator import DeviceOperator
+    mf = make_mf(nao=130, nc=95, no=4, ngrid=3000, xctype="GGA", hyb=0.5)
+    vind, hdiag = osf.gen_tda_operation_sf(mf, isf=1)
+    z = make_trial_vectors(nz, hdiag.size)
+    op = DeviceOperator(mf, "SF_UP")
+    assert rel(op.apply(z), vind(z)) < RTOL

@@ -1,0 +1,54 @@
+"""A.x time per trial-vector count on the headline operator (Davidson steps with few
+new vectors): ms per call and per class (live HIP-event timing) for nvec in --nvecs.
+
+    python tools/nvec_sweep.py [--nvecs 1,2,3,4,6,8,12,16,20] [--reps 3] [--out FILE]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, ".."))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nvecs", default="1,2,3,4,5,6,8,10,12,16,20")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--config", default="H")
+    ap.add_argument("--out", default="gpurun_out/nvec_sweep.json")
+    a = ap.parse_args()
+    import torch
+    import bench
+    args = bench.parse(["--config", a.config])
+    w = bench.device_workload(args, 0, 1, 0)
+    op = w.op
+    rows = []
+    for nv in [int(x) for x in a.nvecs.split(",")]:
+        g = torch.Generator(device="cuda").manual_seed(nv)
+        z = torch.randn((nv, op.dim), dtype=torch.float64, device="cuda", generator=g)
+        out = torch.empty_like(z)
+        op.apply(z, out)
+        torch.cuda.synchronize()
+        op.set_profile(0b111110)
+        cls = {}
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            op.apply(z, out)
+            for k, v in op.profile_stats().items():
+                cls[k] = cls.get(k, 0.0) + v["ms"] / a.reps
+        torch.cuda.synchronize()
+        ms = 1e3 * (time.perf_counter() - t0) / a.reps
+        op.set_profile(0)
+        r = dict(nvec=nv, ms=round(ms, 2), ms_per_vec=round(ms / nv, 2), classes={k: round(v, 2) for k, v in cls.items()})
+        rows.append(r)
+        print(json.dumps(r), flush=True)
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -34,15 +34,18 @@ namespace xt {
 typedef double d4m __attribute__((ext_vector_type(4)));
 
 constexpr int BM_AB = 32;        // virtuals per block (2 MFMA column sub-tiles per wave)
-constexpr int NW = 8;            // waves per block, one trial pair each: 512 threads,
-                                 // 32-point K-tiles, one block per CU (118 KB LDS at TM 7)
+// Block shapes: NW waves (one trial pair each), K-tiles of 4 NW grid points, LDS ~15 NW KB
+// (TM 7); 8 waves per CU in all shapes (256 VGPRs):
+//   NW 8: 512 threads, 32-point K-tiles, one block per CU (the shape for nx >= 8)
+//   NW 4 / 2 / 1: two / four / eight blocks per CU, for Davidson steps with few trial
+//   pairs (nx = 2 nz < 8 would leave most waves of an 8-wave block idle)
 
 // LDS images (doubles), one buffer:
 //   A  [g 32][i 16 TM]        swizzle i ^ 16 (g & 1) for even TM (odd TM: the row pitch
 //                             16 TM = 16 mod 32 doubles already separates the halves)
 //   W  [c 3][g 32][a 32]      swizzle a ^ 16 (g & 1)
 //   R  [g 32][xg 8][c 3]      (broadcast reads)
-template <int TM>
+template <int TM, int NW>
 struct BmLds {
   static constexpr int BK = 4 * NW, XB = NW;
   static constexpr int A = BK * 16 * TM;
@@ -68,14 +71,14 @@ __device__ __forceinline__ double rows4_m(double v) {
 // (TM - 1) + RV); those rows are accumulated on the VALU (RV x 2 FMAs per k-step
 // against the same B fragments, ~55 cycles at RV = 5) instead of a 16-row MFMA
 // sub-tile (2 MFMAs, ~145 cycles), and reduced over the four k-rows once per block.
-template <int TM, int RV = 0>
-__global__ void __launch_bounds__(64 * NW, 1)
+template <int TM, int RV, int NW>
+__global__ void __launch_bounds__(64 * NW)
 k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
             const double* __restrict__ PO, long ldp,
             const double* __restrict__ Wg, long wc, long wg,
             const double* __restrict__ R, long rg,
             double* __restrict__ out, long ldo, long slab) {
-  using L = BmLds<TM>;
+  using L = BmLds<TM, NW>;
   constexpr int BM_BK = L::BK, BM_XB = L::XB, NT = 64 * NW;
   constexpr int R_LD = (L::R + NT - 1) / NT;
   constexpr int PA = 16 * TM;                  // A row length (i)
@@ -316,15 +319,30 @@ static int back_m_splits(int tiles, int nkt, int slots) {
   return best;
 }
 
-// (a 4-wave, two-blocks-per-CU shape measured 167.7 vs 161.4 ms/step: hiding one
-// block's barrier under the other's MFMAs did not pay for twice the barriers and loads)
-struct BackMPlan { int tiles, nkt, splits, kps, used, blocks; };
+// Block shape by the trial pairs: relative cost = blocks per a-tile x NW (the MFMA work)
+// x (1 + the shape's overhead): smaller K-tiles mean more barriers and more PhiO staging
+// per MFMA (NW 4 measured 167.7 vs 161.4 ms/step at nx = 40, i.e. +4 %)
+static int back_m_nw(int nx) {
+  const int nws[4] = {8, 4, 2, 1};
+  const double pen[4] = {0.0, 0.04, 0.1, 0.25};
+  int best = 8;
+  double best_cost = 1e30;
+  for (int k = 0; k < 4; ++k) {
+    const int nw = nws[k];
+    const double cost = (double)((nx + nw - 1) / nw) * nw * (1.0 + pen[k]);
+    if (cost < best_cost - 1e-9) { best_cost = cost; best = nw; }
+  }
+  return best;
+}
+
+struct BackMPlan { int nw, tiles, nkt, splits, kps, used, blocks; };
 static BackMPlan back_m_plan(int nx, int V, int n) {
   BackMPlan p;
-  const int bk = 4 * NW, xb = NW;
+  p.nw = back_m_nw(nx);
+  const int bk = 4 * p.nw, xb = p.nw;
   p.tiles = ((nx + xb - 1) / xb) * ((V + BM_AB - 1) / BM_AB);
   p.nkt = (n + bk - 1) / bk;
-  p.splits = back_m_splits(p.tiles, p.nkt, 256);
+  p.splits = back_m_splits(p.tiles, p.nkt, 256 * (8 / p.nw));
   p.kps = (p.nkt + p.splits - 1) / p.splits;
   p.used = (p.nkt + p.kps - 1) / p.kps;
   p.blocks = p.tiles * p.used;
@@ -339,7 +357,7 @@ size_t xc_back_m_workspace_bytes(int O, int nx, int V, int n) {
 // remainder rows on the VALU for the occupied counts of the BASELINE shapes (O = 33..40:
 // C2, C5; O = 97..104: the headline): RV = O - 16 (TM - 1) <= 8 (<= 6 at TM 7: more
 // spills at 256 VGPRs); otherwise 16-row MFMA tiles throughout
-template <int TM>
+template <int TM, int NW>
 static void launch_back_m(int O, int nx, int V, int n, int kps, int blocks, const double* PO, long ldp,
                           const double* W, long wc, long wg, const double* R, long rg, double* ws, long slab,
                           hipStream_t st) {
@@ -348,13 +366,23 @@ static void launch_back_m(int O, int nx, int V, int n, int kps, int blocks, cons
   const long ldo = (long)nx * V;
   if constexpr (TM == 3 || TM == 7) {
     if (!(TM == 7 && rv > 6)) {
-#define XT_RV(N) case N: hipLaunchKernelGGL((k_xc_back_m<TM, N>), grid, blk, 0, st, O, nx, V, n, kps, PO, ldp, W, wc, \
-                                            wg, R, rg, ws, ldo, slab); return;
+#define XT_RV(N) case N: hipLaunchKernelGGL((k_xc_back_m<TM, N, NW>), grid, blk, 0, st, O, nx, V, n, kps, PO, ldp, W, \
+                                            wc, wg, R, rg, ws, ldo, slab); return;
       switch (rv) { XT_RV(1) XT_RV(2) XT_RV(3) XT_RV(4) XT_RV(5) XT_RV(6) XT_RV(7) XT_RV(8) default: break; }
 #undef XT_RV
     }
   }
-  hipLaunchKernelGGL((k_xc_back_m<TM>), grid, blk, 0, st, O, nx, V, n, kps, PO, ldp, W, wc, wg, R, rg, ws, ldo, slab);
+  hipLaunchKernelGGL((k_xc_back_m<TM, 0, NW>), grid, blk, 0, st, O, nx, V, n, kps, PO, ldp, W, wc, wg, R, rg, ws, ldo,
+                     slab);
+}
+
+template <int NW>
+static void launch_back_m_tm(int TM, int O, int nx, int V, int n, int kps, int blocks, const double* PO, long ldp,
+                             const double* W, long wc, long wg, const double* R, long rg, double* ws, long slab,
+                             hipStream_t st) {
+#define XT_TM(N) case N: launch_back_m<N, NW>(O, nx, V, n, kps, blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+  switch (TM) { XT_TM(1) XT_TM(2) XT_TM(3) XT_TM(4) XT_TM(5) XT_TM(6) XT_TM(7) default: XT_TM(8) }
+#undef XT_TM
 }
 
 int xc_back_m(int O, int nx, int V, int n, const double* PO, long ldp, const double* W, long wc, long wg,
@@ -365,9 +393,12 @@ int xc_back_m(int O, int nx, int V, int n, const double* PO, long ldp, const dou
   const long slab = (long)O * nx * V;
   if (ws_bytes < sizeof(double) * (size_t)p.splits * slab) return XT_ERR_ARG;
   const int TM = (O + 15) / 16;
-#define XT_TM(N) case N: launch_back_m<N>(O, nx, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
-  switch (TM) { XT_TM(1) XT_TM(2) XT_TM(3) XT_TM(4) XT_TM(5) XT_TM(6) XT_TM(7) default: XT_TM(8) }
-#undef XT_TM
+  switch (p.nw) {
+    case 8: launch_back_m_tm<8>(TM, O, nx, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+    case 4: launch_back_m_tm<4>(TM, O, nx, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+    case 2: launch_back_m_tm<2>(TM, O, nx, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+    default: launch_back_m_tm<1>(TM, O, nx, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+  }
   const long total = slab;
   int rb = (int)((total + 255) / 256);
   if (rb > 8192) rb = 8192;

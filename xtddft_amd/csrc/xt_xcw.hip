@@ -53,6 +53,12 @@ __device__ __forceinline__ double rows4(double v) {
   return pair(pair(v, false), true);
 }
 
+// PB trial pairs per block (8, 4, 2, 1; Davidson steps with few new vectors): the
+// H = 8 / PB waves of a pair split each a-tile's k-steps into H even ranges, contract
+// their partial T with the same staged weights (the contraction is linear in T) and
+// their partial sums are added through LDS once at the end -- every wave of the block
+// works when nx < 8, and the weight staging stays one image per a-tile.
+template <int PB>
 __global__ void __launch_bounds__(64 * WXB) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_xc_rho_w(int O, int nx, int V, int n,
            const double* __restrict__ PO, long ldp,
@@ -84,12 +90,16 @@ k_xc_rho_w(int O, int nx, int V, int n,
   }
   // (trial-pair sets of one g-tile side by side instead, sharing its gradient weights
   // in L2: neutral, 168.1-168.3 vs 168.2-168.6 ms/step)
+  constexpr int H = WXB / PB;                  // waves per pair
   const int gt = lid % ntg, xs = lid / ntg;
-  const int g0 = gt * GB, x0 = xs * WXB;
-  const int xg = x0 + wave;                    // this wave's trial pair
-  const bool wave_on = xg < nx;
+  const int g0 = gt * GB, x0 = xs * PB;
+  const int pl = wave % PB, h = wave / PB;
+  const int xg = x0 + pl;                      // this wave's trial pair
   const int nat = (V + WA - 1) / WA;
   const int KS = KI / 4;
+  // this wave's k-steps of every a-tile: [s_lo, s_hi), even bounds (the ring phase stays even)
+  const int s_lo = 2 * ((h * (KS / 2)) / H), s_hi = 2 * (((h + 1) * (KS / 2)) / H);
+  const bool wave_on = xg < nx && s_hi > s_lo;
 
   // ---- PhiO tile -> LDS (once) ----------------------------------------------
   for (int p = tid; p < KI * GB; p += NT) {
@@ -122,20 +132,22 @@ k_xc_rho_w(int O, int nx, int V, int n,
   const double* zb = Z + (long)(wave_on ? xg : 0) * zx + r16 + (long)q * zi;
   double zq[ZD][TMA];
   const long zstep = 4 * zi;
-  const double* zn = zb;                       // next k-step to load: a-tile za, k-step zs
-  int zs = 0, za = 0;
-  // advance to the next k-step; past the a-tile's last k-step the pointer jumps to the
-  // next tile's first row (the last tile repeats itself: those loads are never
-  // consumed).  An if/else, which splits the unrolled K loop into one basic block per
-  // k-step (a select-based form with one block per 4 k-steps measured 4 % slower).
+  const double* zn = zb + s_lo * zstep;        // next k-step to load: a-tile za, k-step zs
+  int zs = s_lo, za = 0;
+  // advance to the next k-step; past the wave's last k-step of an a-tile the pointer jumps
+  // to its first k-step of the next tile (the last tile repeats itself: those loads are
+  // never consumed).  An if/else, which splits the unrolled K loop into one basic block
+  // per k-step (a select-based form with one block per 4 k-steps measured 4 % slower).
   auto load_z = [&](int slot) XT_INLINE {
 #pragma unroll
     for (int t = 0; t < TMA; ++t) zq[slot][t] = zn[16 * t];
-    if (++zs == KS) { zs = 0; za = za + 1 < nat ? za + 1 : za; zn = zb + za * WA; }
+    if (++zs == s_hi) { zs = s_lo; za = za + 1 < nat ? za + 1 : za; zn = zb + za * WA + s_lo * zstep; }
     else zn += zstep;
   };
+  if (wave_on) {
 #pragma unroll
-  for (int d = 0; d < ZD; ++d) load_z(d);
+    for (int d = 0; d < ZD; ++d) load_z(d);
+  }
 
   d4w acc[TMA][TNG];
   double racc[TNG][3];
@@ -178,7 +190,7 @@ k_xc_rho_w(int O, int nx, int V, int n,
   // k-steps [s0, s1) of a-tile at (s0 even: the ring phase stays even)
   auto krange = [&](int at, int s0, int s1) XT_INLINE {
     static_assert(ZD == 4, "ring phases");
-    const int ph = (int)(((long)at * KS + s0) % ZD);
+    const int ph = (int)(((long)at * (s_hi - s_lo) + s0 - s_lo) % ZD);
     if (ph == 0) kloop(std::integral_constant<int, 0>{}, s0, s1);
     else         kloop(std::integral_constant<int, 2>{}, s0, s1);
   };
@@ -191,7 +203,7 @@ k_xc_rho_w(int O, int nx, int V, int n,
 #pragma unroll
       for (int j = 0; j < TNG; ++j) acc[t][j] = (d4w){0.0, 0.0, 0.0, 0.0};
     if (wave_on) {
-      krange(at, 0, KS);
+      krange(at, s_lo, s_hi);
       // contraction with the a-tile's weights: acc[t][j][r] = T[a = 16 t + q + 4 r][g = 16 j + r16].
       // Half a row (t, r) of weights at a time, the next half's reads issued before this
       // half's FMAs (two 6-value buffers; unfenced, the compiler hoists all 96 reads and
@@ -229,7 +241,28 @@ k_xc_rho_w(int O, int nx, int V, int n,
     if (at + 1 < nat) store_w(buf ^ 1, at + 1);
     __syncthreads();
   }
-  if (!wave_on) return;
+  if constexpr (H > 1) {
+    // the H waves of a pair hold partial sums over disjoint k-ranges: add them through
+    // LDS (the weight buffers are free after the last barrier)
+    double* red = sW;                            // [wave][j c][lane]
+    if (h > 0) {
+#pragma unroll
+      for (int j = 0; j < TNG; ++j)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) red[(wave * 3 * TNG + j * 3 + c) * 64 + lane] = racc[j][c];
+    }
+    __syncthreads();
+    if (h == 0) {
+      for (int hh = 1; hh < H; ++hh) {
+        const int w2 = pl + hh * PB;
+#pragma unroll
+        for (int j = 0; j < TNG; ++j)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) racc[j][c] += red[(w2 * 3 * TNG + j * 3 + c) * 64 + lane];
+      }
+    }
+  }
+  if (h != 0 || xg >= nx) return;
 #pragma unroll
   for (int j = 0; j < TNG; ++j) {
     const int g = g0 + 16 * j + r16;
@@ -251,16 +284,30 @@ static size_t rho_w_lds(int O) {
 
 size_t xc_rho_w_lds_bytes(int O) { return rho_w_lds(O); }
 
-// the 160 KB dynamic-LDS attribute, set once per device (thread-safe)
-static void rho_w_lds_attribute() {
+// the 160 KB dynamic-LDS attribute, set once per device and kernel (thread-safe)
+template <typename K>
+static void lds_attribute(K kern, int slot) {
   static std::mutex mu;
-  static unsigned long long done = 0;
+  static unsigned long long done[4] = {0, 0, 0, 0};
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(mu);
-  if (dev < 64 && (done >> dev & 1ull)) return;
-  (void)hipFuncSetAttribute((const void*)k_xc_rho_w, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (dev < 64) done |= 1ull << dev;
+  if (dev < 64 && (done[slot] >> dev & 1ull)) return;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (dev < 64) done[slot] |= 1ull << dev;
+}
+
+// pairs per block: relative block time ~ PB / 8 (the k-steps each wave runs) + 0.13 (the
+// per-a-tile contraction, staging and barrier, ~21 of 168 ms at PB 8), times the blocks
+// per grid tile; the cheapest wins
+static int rho_w_pb(int nx) {
+  int best = 8;
+  double best_cost = 1e30;
+  for (int pb = 8; pb >= 1; pb /= 2) {
+    const double cost = (double)((nx + pb - 1) / pb) * (pb / 8.0 + 0.13);
+    if (cost < best_cost - 1e-9) { best_cost = cost; best = pb; }
+  }
+  return best;
 }
 
 int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const double* Z, long zi, long zx,
@@ -268,11 +315,18 @@ int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const doub
   if (O <= 0 || nx <= 0 || V <= 0 || n <= 0) return 0;
   const size_t lds = rho_w_lds(O);
   if (lds > 160 * 1024) return XT_ERR_ARG;
-  rho_w_lds_attribute();
   constexpr int GB = 16 * TNG;
-  const int blocks = ((n + GB - 1) / GB) * ((nx + WXB - 1) / WXB);
-  hipLaunchKernelGGL(k_xc_rho_w, dim3(blocks), dim3(64 * WXB), lds, st, O, nx, V, n, PO, ldp, Z, zi, zx, W, wc, wg,
-                     R, rg);
+  const int ntg = (n + GB - 1) / GB;
+  const int pb = rho_w_pb(nx);
+  const int blocks = ntg * ((nx + pb - 1) / pb);
+#define XT_W(PBV, S)                                                                                       \
+  case PBV:                                                                                                \
+    lds_attribute(k_xc_rho_w<PBV>, S);                                                                     \
+    hipLaunchKernelGGL((k_xc_rho_w<PBV>), dim3(blocks), dim3(64 * WXB), lds, st, O, nx, V, n, PO, ldp, Z, \
+                       zi, zx, W, wc, wg, R, rg);                                                          \
+    break;
+  switch (pb) { XT_W(8, 0) XT_W(4, 1) XT_W(2, 2) default: XT_W(1, 3) }
+#undef XT_W
   return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
 }
 

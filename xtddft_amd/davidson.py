@@ -13,7 +13,8 @@ returning the 4-tuple ``(conv, e, x, icyc)`` its callers unpack
 * ``_qr`` orthonormalises a block with two host round trips: Gram-Schmidt
   on the host in the coefficient space of the Gram matrix (same order and
   drop rule ``norm**2 > lindep`` as the reference's vector-by-vector
-  modified Gram-Schmidt), then one Cholesky-QR pass on the device;
+  modified Gram-Schmidt), then one Cholesky-QR pass on the device; nearly
+  dependent blocks fall back to the vector-by-vector form on the device;
   ``_normalize_xt_`` projects out the subspace with two passes of classical
   Gram-Schmidt as GEMMs (CGS2).  Equal in exact arithmetic to the
   reference's orthogonalisation, orthogonal to round-off.
@@ -120,10 +121,11 @@ def _gram_gs(g, lindep):
     """Gram-Schmidt in coefficient space: rows of C (kept x n) with C x
     orthonormal, processing the rows of x in order and dropping a row whose
     residual norm**2 <= lindep (PySCF _qr's rule) -- from the Gram matrix
-    g = x x^T alone."""
+    g = x x^T alone.  Returns (C, smallest kept norm**2)."""
     n = g.shape[0]
     c = np.zeros((n, n))
     kept = 0
+    nmin = np.inf
     for i in range(n):
         r = np.zeros(n)
         r[i] = 1.0
@@ -134,7 +136,31 @@ def _gram_gs(g, lindep):
         if nrm2 > lindep:
             c[kept] = r / np.sqrt(nrm2)
             kept += 1
-    return c[:kept]
+            nmin = min(nmin, nrm2)
+    return c[:kept], nmin
+
+
+# Below this residual norm**2 the Gram-matrix route loses the accuracy the drop rule
+# needs (its rounding grows like eps / norm**2): orthonormalise vector by vector instead.
+GRAM_SAFE_NORM2 = 1e-8
+
+
+def _qr_vectorwise(dev, x, lindep):
+    """PySCF _qr row by row on the device: each row has the kept rows projected out
+    (two classical Gram-Schmidt passes), is dropped when its residual norm**2 <=
+    lindep and normalised otherwise.  One host round trip per row."""
+    torch = dev.torch
+    n, dim = x.shape
+    out = torch.empty_like(x)
+    kept = 0
+    for i in range(n):
+        v = x[i:i + 1].clone()
+        dev.project_out(v, out[:kept], kept)
+        nrm2 = float(dev.norms2(v)[0])
+        if nrm2 > lindep:
+            out[kept] = v[0] / np.sqrt(nrm2)
+            kept += 1
+    return out[:kept]
 
 
 def _qr(dev, x, lindep):
@@ -143,7 +169,9 @@ def _qr(dev, x, lindep):
     of one per vector: the Gram matrix x x^T (device GEMM) drives Gram-Schmidt
     on the host in coefficient space (same order, same drop rule), Q1 = C x on
     the device, then one Cholesky-QR pass Q = L^-1 Q1 (L L^T = Q1 Q1^T)
-    restores orthogonality to round-off (CholQR2 pattern)."""
+    restores orthogonality to round-off (CholQR2 pattern).  Nearly dependent
+    rows (a kept residual norm**2 below GRAM_SAFE_NORM2) or a failed Cholesky take
+    the vector-by-vector path (``_qr_vectorwise``)."""
     torch = dev.torch
     n, dim = x.shape
     if n == 0:
@@ -151,17 +179,23 @@ def _qr(dev, x, lindep):
     x = x.contiguous()
     g = torch.empty((n, n), dtype=torch.float64, device=dev.device)
     dev.gemm(0, 1, n, n, dim, 1.0, x, dim, x, dim, 0.0, g, n)
-    c = _gram_gs(g.cpu().numpy(), lindep)
+    c, nmin = _gram_gs(g.cpu().numpy(), lindep)
     k = c.shape[0]
     if k == 0:
         return x[:0]
+    if nmin < GRAM_SAFE_NORM2:
+        return _qr_vectorwise(dev, x, lindep)
     ct = torch.as_tensor(np.ascontiguousarray(c), device=dev.device)
     q = torch.empty((k, dim), dtype=torch.float64, device=dev.device)
     dev.gemm(0, 0, k, dim, n, 1.0, ct, n, x, dim, 0.0, q, dim)
     g2 = torch.empty((k, k), dtype=torch.float64, device=dev.device)
     dev.gemm(0, 1, k, k, dim, 1.0, q, dim, q, dim, 0.0, g2, k)
     g2h = g2.cpu().numpy()
-    linv = scipy.linalg.solve_triangular(np.linalg.cholesky(0.5 * (g2h + g2h.T)), np.eye(k), lower=True)
+    try:
+        low = np.linalg.cholesky(0.5 * (g2h + g2h.T))
+    except np.linalg.LinAlgError:
+        return _qr_vectorwise(dev, x, lindep)
+    linv = scipy.linalg.solve_triangular(low, np.eye(k), lower=True)
     lt = torch.as_tensor(np.ascontiguousarray(linv), device=dev.device)
     out = torch.empty_like(q)
     dev.gemm(0, 0, k, dim, k, 1.0, lt, k, q, dim, 0.0, out, dim)
@@ -223,6 +257,7 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
                 raise LinearDependenceError('Initial guess is empty or zero' if icyc == 0 else
                                             'No more linearly independent basis were found.')
             x0 = None
+            max_dx_last = 1e9            # Davidson.py:168
         elif xt.shape[0] > 1:
             xt = _qr(dev, xt, lindep)[:40]
         axt = aop(xt)
