@@ -112,3 +112,14 @@ def hf_cluster(n: int, charge: int = 1, spin: int = 1, spacing: float = 2.9):
         atoms.append(("F", tuple(site)))
         atoms.append(("H", tuple(site + 0.917 * axes[i % len(axes)])))
     return M(atoms, basis=hf_pol_basis(), charge=charge, spin=spin)
+
+
+def hf_cluster_radical(n: int, spacing: float = 2.9):
+    """(HF)_n + an H atom 2.5 A beyond the last lattice site: a doublet whose open
+    shell is localised (the cluster stays closed-shell), 23 n + 2 AOs in hf_pol_basis."""
+    import numpy as np
+    mol = hf_cluster(n, charge=0, spin=0, spacing=spacing)
+    atoms = [(el, tuple(c * 0.52917721092)) for el, c in zip(mol.elements, mol.atom_coords())]
+    far = np.array(atoms[-2][1]) + np.array([2.5, 2.5, 0.0])
+    atoms.append(("H", tuple(far)))
+    return M(atoms, basis=hf_pol_basis(), charge=0, spin=1)

@@ -1,5 +1,6 @@
-"""End to end on the device for a >= 300-AO molecule: (HF)_n cluster cation,
-6-31G + d + f on F (tests/molecules.py hf_cluster), ROKS B3LYP with exact J/K from
+"""End to end on the device for a >= 300-AO molecule: (HF)_n cluster plus an H atom
+(a doublet with a localised open shell), 6-31G + d + f on F (tests/molecules.py
+hf_cluster_radical), ROKS B3LYP with exact J/K from
 the integral-direct Cholesky factor (no 4-index array), device integrals and AO
 values, then X-TDA 20 roots through the device operator and Davidson.
 
@@ -31,12 +32,12 @@ def main():
     ap.add_argument("--out", default="gpurun_out/frontend_run.json")
     a = ap.parse_args()
     import torch
-    from molecules import hf_cluster
+    from molecules import hf_cluster_radical
     from xtddft_amd.qc import ROKS
     from xtddft_amd.xtda import XTDA
-    rec = dict(molecule=f"(HF){a.n}+ doublet, 6-31G + d,f on F", xc=a.xc, chol_tol=a.tol)
+    rec = dict(molecule=f"(HF){a.n} + H doublet, 6-31G + d,f on F", xc=a.xc, chol_tol=a.tol)
     t0 = time.perf_counter()
-    mol = hf_cluster(a.n)
+    mol = hf_cluster_radical(a.n)
     rec.update(nao=mol.nao, nshell=len(mol.shells), natm=mol.natm, mole_s=time.perf_counter() - t0)
     mf = ROKS(mol, a.xc)
     mf.conv_tol = a.conv

@@ -321,10 +321,10 @@ static int back_m_splits(int tiles, int nkt, int slots) {
 
 // Block shape by the trial pairs: relative cost = blocks per a-tile x NW (the MFMA work)
 // x (1 + the shape's overhead): smaller K-tiles mean more barriers and more PhiO staging
-// per MFMA (NW 4 measured 167.7 vs 161.4 ms/step at nx = 40, i.e. +4 %)
+// per MFMA (per pair, relative to NW 8 at nx = 8: NW 4 +12 %, NW 2 +75 %)
 static int back_m_nw(int nx) {
   const int nws[4] = {8, 4, 2, 1};
-  const double pen[4] = {0.0, 0.04, 0.1, 0.25};
+  const double pen[4] = {0.0, 0.12, 0.75, 2.0};   // measured at the headline shape
   int best = 8;
   double best_cost = 1e30;
   for (int k = 0; k < 4; ++k) {

@@ -68,8 +68,10 @@ k_xc_rho_w(int O, int nx, int V, int n,
   constexpr int GB = 16 * TNG;                 // grid points per block
   constexpr int W_IMG = 3 * WA * GB;           // one weight buffer (doubles)
   constexpr int NT = 64 * WXB;                 // threads per block
-  constexpr int W_LD = W_IMG / NT;             // weight elements staged per thread
-  static_assert(W_IMG % NT == 0, "weight staging map");
+  // each a-tile's weights are staged in two halves (loaded before / stored after each half
+  // of the K loop), 6 staging registers instead of 12
+  constexpr int W_LD = W_IMG / NT / 2;         // weight elements staged per thread and half
+  static_assert(W_IMG % (2 * NT) == 0, "weight staging map");
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int KI = (O + 7) & ~7;                 // occupied rows in the image (k-steps even)
   double* sP = sm;                             // [KI][GB]
@@ -98,8 +100,8 @@ k_xc_rho_w(int O, int nx, int V, int n,
   const int nat = (V + WA - 1) / WA;
   const int KS = KI / 4;
   // this wave's k-steps of every a-tile: [s_lo, s_hi), even bounds (the ring phase stays even)
-  const int s_lo = 2 * ((h * (KS / 2)) / H), s_hi = 2 * (((h + 1) * (KS / 2)) / H);
-  const bool wave_on = xg < nx && s_hi > s_lo;
+  const int s_lo = H == 1 ? 0 : 2 * ((h * (KS / 2)) / H), s_hi = H == 1 ? KS : 2 * (((h + 1) * (KS / 2)) / H);
+  const bool wave_on = H == 1 ? xg < nx : (xg < nx && s_hi > s_lo);
 
   // ---- PhiO tile -> LDS (once) ----------------------------------------------
   for (int p = tid; p < KI * GB; p += NT) {
@@ -109,22 +111,24 @@ k_xc_rho_w(int O, int nx, int V, int n,
   }
   // ---- weights of a-tile `at` (global -> registers -> LDS) -------------------
   double rw[W_LD];
-  auto load_w = [&](int at) XT_INLINE {
+  auto load_w = [&](int at, int ph) XT_INLINE {
 #pragma unroll
     for (int e = 0; e < W_LD; ++e) {
-      const int p = tid + NT * e, c = p / (WA * GB), g = (p / WA) % GB, a = p % WA;
+      const int p = tid + NT * (e + ph * W_LD), c = p / (WA * GB), g = (p / WA) % GB, a = p % WA;
       rw[e] = Wg[c * wc + (long)(g0 + g) * wg + min(at * WA + a, V - 1)];
     }
   };
-  auto store_w = [&](int buf, int at) XT_INLINE {
+  auto store_w = [&](int buf, int at, int ph) XT_INLINE {
 #pragma unroll
     for (int e = 0; e < W_LD; ++e) {
-      const int p = tid + NT * e, c = p / (WA * GB), g = (p / WA) % GB, a = p % WA;
+      const int p = tid + NT * (e + ph * W_LD), c = p / (WA * GB), g = (p / WA) % GB, a = p % WA;
       sW[buf * W_IMG + (c * WA + a) * GB + (g ^ swz(a))] = at * WA + a < V ? rw[e] : 0.0;
     }
   };
-  load_w(0);
-  store_w(0, 0);
+  load_w(0, 0);
+  store_w(0, 0, 0);
+  load_w(0, 1);
+  store_w(0, 0, 1);
 
   // ---- Zp ring: k-step u of the whole a loop (a-tile u / KS, k-step u % KS) ----
   // lane (q, r16) loads rows i = 4 s + q (past O: zeroed slack rows of Zp) of
@@ -132,7 +136,7 @@ k_xc_rho_w(int O, int nx, int V, int n,
   const double* zb = Z + (long)(wave_on ? xg : 0) * zx + r16 + (long)q * zi;
   double zq[ZD][TMA];
   const long zstep = 4 * zi;
-  const double* zn = zb + s_lo * zstep;        // next k-step to load: a-tile za, k-step zs
+  const double* zn = H == 1 ? zb : zb + s_lo * zstep;   // next k-step to load: a-tile za, k-step zs
   int zs = s_lo, za = 0;
   // advance to the next k-step; past the wave's last k-step of an a-tile the pointer jumps
   // to its first k-step of the next tile (the last tile repeats itself: those loads are
@@ -141,10 +145,15 @@ k_xc_rho_w(int O, int nx, int V, int n,
   auto load_z = [&](int slot) XT_INLINE {
 #pragma unroll
     for (int t = 0; t < TMA; ++t) zq[slot][t] = zn[16 * t];
-    if (++zs == s_hi) { zs = s_lo; za = za + 1 < nat ? za + 1 : za; zn = zb + za * WA + s_lo * zstep; }
-    else zn += zstep;
+    if constexpr (H == 1) {
+      if (++zs == KS) { zs = 0; za = za + 1 < nat ? za + 1 : za; zn = zb + za * WA; }
+      else zn += zstep;
+    } else {
+      if (++zs == s_hi) { zs = s_lo; za = za + 1 < nat ? za + 1 : za; zn = zb + za * WA + s_lo * zstep; }
+      else zn += zstep;
+    }
   };
-  if (wave_on) {
+  if (H == 1 || wave_on) {   // (a wave with no k-steps must not walk the ring)
 #pragma unroll
     for (int d = 0; d < ZD; ++d) load_z(d);
   }
@@ -157,13 +166,18 @@ k_xc_rho_w(int O, int nx, int V, int n,
     for (int c = 0; c < 3; ++c) racc[j][c] = 0.0;
 
   const int p_lane = q * GB;                   // B image: row 4 s + q, column (16 j + r16) ^ swz
-  // one k-step from ring slot `slot` (a compile-time constant after unrolling)
-  auto step = [&](int s, int slot) XT_INLINE {
-    const int i = 4 * s + q;
-    const int sw = swz(i);
-    double bf[TNG];
+  // B fragments one k-step ahead: step s reads bq[s & 1] and loads step s + 1's into
+  // bq[(s + 1) & 1] before its MFMAs, so their LDS latency hides under this step's
+  // matrix work (a read past the last k-step lands in the weight image: unused)
+  double bq[2][TNG];
+  auto bload = [&](int s, double* dst) XT_INLINE {
+    const int sw = swz(4 * s + q);
 #pragma unroll
-    for (int j = 0; j < TNG; ++j) bf[j] = sP[p_lane + 4 * s * GB + ((16 * j + r16) ^ sw)];
+    for (int j = 0; j < TNG; ++j) dst[j] = sP[p_lane + 4 * s * GB + ((16 * j + r16) ^ sw)];
+  };
+  // one k-step from ring slot `slot` and B buffer `bb` (compile-time after unrolling)
+  auto step = [&](int s, int slot, int bb) XT_INLINE {
+    bload(s + 1, bq[bb ^ 1]);
     double af[TMA];
 #pragma unroll
     for (int t = 0; t < TMA; ++t) af[t] = zq[slot][t];
@@ -172,36 +186,42 @@ k_xc_rho_w(int O, int nx, int V, int n,
     for (int t = 0; t < TMA; ++t)
 #pragma unroll
       for (int j = 0; j < TNG; ++j)
-        acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t], bf[j], acc[t][j], 0, 0, 0);
+        acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t], bq[bb][j], acc[t][j], 0, 0, 0);
   };
   // the K loop of one a-tile whose first k-step sits in ring slot PH (KS is even, so
   // PH is even); the slots stay compile-time constants inside each unrolled group
   auto kloop = [&](auto PH, int s0, int s1) XT_INLINE {
     constexpr int P = decltype(PH)::value;
+    bload(s0, bq[0]);
     int s = s0;
     for (; s + ZD <= s1; s += ZD) {
 #pragma unroll
-      for (int d = 0; d < ZD; ++d) step(s + d, (P + d) % ZD);
+      for (int d = 0; d < ZD; ++d) step(s + d, (P + d) % ZD, d & 1);
     }
 #pragma unroll
     for (int d = 0; d < ZD; ++d)
-      if (s + d < s1) step(s + d, (P + d) % ZD);
+      if (s + d < s1) step(s + d, (P + d) % ZD, d & 1);
   };
   // k-steps [s0, s1) of a-tile at (s0 even: the ring phase stays even)
   auto krange = [&](int at, int s0, int s1) XT_INLINE {
     static_assert(ZD == 4, "ring phases");
-    const int ph = (int)(((long)at * (s_hi - s_lo) + s0 - s_lo) % ZD);
+    const int ph = H == 1 ? (int)(((long)at * KS + s0) % ZD) : (int)(((long)at * (s_hi - s_lo) + s0 - s_lo) % ZD);
     if (ph == 0) kloop(std::integral_constant<int, 0>{}, s0, s1);
     else         kloop(std::integral_constant<int, 2>{}, s0, s1);
   };
   __syncthreads();
+  const int s_mid = s_lo + (((s_hi - s_lo) / 2) & ~1);
   for (int at = 0; at < nat; ++at) {
     const int buf = at & 1;
-    if (at + 1 < nat) load_w(at + 1);
+    if (at + 1 < nat) load_w(at + 1, 0);
 #pragma unroll
     for (int t = 0; t < TMA; ++t)
 #pragma unroll
       for (int j = 0; j < TNG; ++j) acc[t][j] = (d4w){0.0, 0.0, 0.0, 0.0};
+    if (at + 1 < nat) {
+      store_w(buf ^ 1, at + 1, 0);
+      load_w(at + 1, 1);
+    }
     if (wave_on) {
       krange(at, s_lo, s_hi);
       // contraction with the a-tile's weights: acc[t][j][r] = T[a = 16 t + q + 4 r][g = 16 j + r16].
@@ -238,7 +258,7 @@ k_xc_rho_w(int O, int nx, int V, int n,
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (at + 1 < nat) store_w(buf ^ 1, at + 1);
+    if (at + 1 < nat) store_w(buf ^ 1, at + 1, 1);
     __syncthreads();
   }
   if constexpr (H > 1) {

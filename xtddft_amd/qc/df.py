@@ -114,7 +114,13 @@ class DF:
     def cderi_lr(self, omega: float):
         """The long-range factor of erf(omega r12)/r12 (PySCF ``with_df.range_coulomb``:
         3-index and 2-index integrals both attenuated), the ``cderi_lr`` of a
-        range-separated mean field (MeanField, XTDA.py:527-539)."""
+        range-separated mean field (MeanField, XTDA.py:527-539).
+
+        A standalone integral capability: no range-separated functional is built
+        (``xc.rsh_and_hybrid_coeff`` returns omega = 0 for every functional here), so
+        ``_meanfield`` never fills ``cderi_lr`` and the operator's long-range exchange
+        (``operator.py``) is driven only by callers that supply the factor; its
+        end-to-end parity is unpinned."""
         self.build()
         j3 = self.mol.int3c2e(self.auxmol, device=self.device, omega=omega)
         return cholesky_cderi(j3, self.auxmol.int2c2e(omega=omega))

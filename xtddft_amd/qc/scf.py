@@ -132,6 +132,9 @@ class _SCFBase:
             self.ao = mol.eval_ao(self.grids.coords, deriv=1 if self.xctype == "GGA" else 0, device=dev)
             if self.ao.ndim == 2:
                 self.ao = self.ao[None]
+            if dev is not None:
+                import torch
+                torch.cuda.synchronize(dev)
             self.timings["eval_ao_s"] = time.perf_counter() - t0
         if self._device is not None:
             from .device import DeviceEngine
