@@ -31,6 +31,7 @@ extern "C" {
 #define XT_XC_NONE 0       /* pure Hartree-Fock response (XTDA.py:546-554)                 */
 #define XT_XC_LDA 1
 #define XT_XC_GGA 2
+#define XT_XC_MGGA 3       /* meta-GGA: (rho, grad rho, tau) kernel, XTDA.py:239-276 / nr_uks_fxc   */
 
 typedef struct xt_ctx xt_ctx;
 
@@ -99,9 +100,10 @@ int xt_set_jk_eri8(xt_ctx* ctx, const double* eri_s8, int which, double tol,
    found by xt_set_jk_eri8) and the full Cholesky rank of the last
    xt_set_jk_eri8 (before sharding). */
 int xt_naux(const xt_ctx* ctx, int* naux_local, int* chol_rank);
-/* AO values on the grid (ncomp x ngrid x nao; ncomp = 1 LDA / 4 GGA),
-   weights (ngrid) and the kernel: UKS fxc (2 x ncomp x 2 x ncomp x ngrid,
-   un-weighted) for XTDA/UTDA, or the weighted ALDA0 kernel (ngrid) for SF/XSF.
+/* AO values on the grid (ncomp x ngrid x nao; ncomp = 1 LDA / 4 GGA and MGGA),
+   weights (ngrid) and the kernel: UKS fxc (2 x nk x 2 x nk x ngrid, un-weighted;
+   nk = 1 LDA, 4 GGA, 5 MGGA with tau = 1/2 sum |grad phi|^2 last) for XTDA/UTDA, or
+   the weighted ALDA0 kernel (ngrid) for SF/XSF.
    Replaces ni.cache_xc_kernel / cache_xc_kernel_sf (XTDA.py:504, SF_TDA.py:39-88)
    and the per-call grid loop of ni.nr_uks_fxc / nr_uks_fxc_sf_tda
    (XTDA.py:514, SF_TDA.py:90-160). */

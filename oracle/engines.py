@@ -7,7 +7,8 @@ Restates what PySCF computes inside the reference's ``vresp`` closures:
   ``vk = einsum('ijkl,jk->il', eri, dm)`` (call sites XTDA.py:518-543,
   SF_TDA.py:273-281, XSF_TDA.py:996).
 * ``nr_uks_fxc`` -- ``ni.nr_uks_fxc`` for hermi=0 densities (XTDA.py:514):
-  rho1 from ``eval_rho`` (GGA gradient terms both ways for non-hermitian dm),
+  rho1 from ``eval_rho`` (GGA gradient terms both ways for non-hermitian dm; MGGA
+  tau1 = 1/2 sum_c d_c phi D d_c phi, V += 1/2 sum_c d_c phi^T w_tau d_c phi),
   ``wv = w * einsum('axg,axbyg->byg', rho1, fxc)``, then for GGA
   ``wv[0]*=.5; V = ao0^T (sum_y ao_y wv_y); V += V^T``.
 * ``nr_uks_fxc_sf_tda`` -- the reference's own ALDA0 spin-flip kernel
@@ -135,28 +136,36 @@ def get_k_total(mf, dms):
 
 
 def _eval_rho(ao, dm, xctype):
-    """PySCF eval_rho for a non-hermitian dm (hermi=0)."""
+    """PySCF eval_rho for a non-hermitian dm (hermi=0); MGGA adds
+    tau = 1/2 sum_c sum_pq d_c phi_p D_pq d_c phi_q."""
     c0 = ao[0] @ dm                       # c0[g,q] = sum_p phi_p D_pq
     rho0 = np.einsum('gq,gq->g', ao[0], c0)
     if xctype == 'LDA':
         return rho0[None]
     c1 = ao[0] @ dm.T                     # c1[g,q] = sum_p phi_p D_qp
-    rho = np.empty((4, ao.shape[1]))
+    rho = np.empty((5 if xctype == 'MGGA' else 4, ao.shape[1]))
     rho[0] = rho0
     for i in range(1, 4):
         rho[i] = np.einsum('gq,gq->g', ao[i], c0) + np.einsum('gq,gq->g', c1, ao[i])
+    if xctype == 'MGGA':
+        rho[4] = 0.5 * sum(np.einsum('gq,gq->g', ao[i] @ dm, ao[i]) for i in range(1, 4))
     return rho
 
 
 def _wv_to_vmat(ao, wv, xctype):
-    """V_mu,nu from weighted potential wv (PySCF _dot_ao_ao / hermi_sum for GGA)."""
+    """V_mu,nu from weighted potential wv (PySCF _dot_ao_ao / hermi_sum for GGA;
+    MGGA adds 1/2 sum_c d_c phi^T w_tau d_c phi)."""
     if xctype == 'LDA':
         return ao[0].T @ (wv[0][:, None] * ao[0])
     wv = wv.copy()
     wv[0] *= .5
-    aow = np.einsum('yg,ygq->gq', wv, ao)
+    aow = np.einsum('yg,ygq->gq', wv[:4], ao[:4])
     v = ao[0].T @ aow
-    return v + v.T
+    v = v + v.T
+    if xctype == 'MGGA':
+        for i in range(1, 4):
+            v += 0.5 * ao[i].T @ (wv[4][:, None] * ao[i])
+    return v
 
 
 def nr_uks_fxc(mf, dms):
@@ -164,12 +173,13 @@ def nr_uks_fxc(mf, dms):
     grids, fxc, xctype = mf.grids, mf.fxc, mf.xctype
     dms = np.asarray(dms)
     nz, nao = dms.shape[1], dms.shape[-1]
-    ncomp = 1 if xctype == 'LDA' else 4
+    ncomp = {'LDA': 1, 'GGA': 4, 'MGGA': 5}[xctype]
+    nao_c = min(ncomp, 4)                 # AO values + gradients (tau needs no more)
     vmat = np.zeros((2, nz, nao, nao))
     ng = grids.ngrid
     for g0 in range(0, ng, GRID_BLOCK):
         g1 = min(ng, g0 + GRID_BLOCK)
-        ao = grids.ao[:ncomp, g0:g1]
+        ao = grids.ao[:nao_c, g0:g1]
         w = grids.weights[g0:g1]
         f = fxc[:, :ncomp, :, :ncomp, g0:g1]
         for i in range(nz):

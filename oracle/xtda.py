@@ -7,7 +7,7 @@
 * ``get_init_guess`` restates XTDA.py:700-734, ``get_precond`` XTDA.py:736-744.
 * ``full_diag_matrix`` restates the explicit A of ``XTDA.full_diag``
   (XTDA.py:56-400) with MO integrals from the same DF factor and the
-  explicit XC kernel loops (LDA XTDA.py:178-207, GGA 208-238) -- an
+  explicit XC kernel loops (LDA XTDA.py:178-207, GGA 208-238, MGGA 239-276) -- an
   independent code path used to pin ``vind``.
 """
 from __future__ import annotations
@@ -191,7 +191,7 @@ def full_diag_matrix(mf):
         aa -= np.einsum('ijba->iajb', eri_aa[:nocc_a, :nocc_a, nocc_a:, nocc_a:]) * c_lr
         bb -= np.einsum('ijba->iajb', eri_bb[:nocc_b, :nocc_b, nocc_b:, nocc_b:]) * c_lr
 
-    if mf.xctype in ('LDA', 'GGA'):
+    if mf.xctype in ('LDA', 'GGA', 'MGGA'):
         ao = mf.grids.ao
         w = mf.grids.weights
         fxc = mf.fxc
@@ -216,6 +216,11 @@ def full_diag_matrix(mf):
             rho_ov_b = np.einsum('xri,ra->xria', rho_o_b, rho_v_b[0])
             rho_ov_a[1:4] += np.einsum('ri,xra->xria', rho_o_a[0], rho_v_a[1:4])
             rho_ov_b[1:4] += np.einsum('ri,xra->xria', rho_o_b[0], rho_v_b[1:4])
+            if mf.xctype == 'MGGA':     # tau_ov = 1/2 sum_c d_c phi_i d_c phi_a (XTDA.py:256-259)
+                tau_ov_a = np.einsum('xri,xra->ria', rho_o_a[1:4], rho_v_a[1:4]) * .5
+                tau_ov_b = np.einsum('xri,xra->ria', rho_o_b[1:4], rho_v_b[1:4]) * .5
+                rho_ov_a = np.vstack([rho_ov_a, tau_ov_a[np.newaxis]])
+                rho_ov_b = np.vstack([rho_ov_b, tau_ov_b[np.newaxis]])
             w_ov_aa = np.einsum('xyr,xria->yria', wfxc[0, :, 0], rho_ov_a)
             w_ov_ab = np.einsum('xyr,xria->yria', wfxc[0, :, 1], rho_ov_a)
             w_ov_bb = np.einsum('xyr,xria->yria', wfxc[1, :, 1], rho_ov_b)

@@ -32,7 +32,16 @@ def hf_mol():
 @lru_cache(maxsize=None)
 def hf_scf(kind: str):
     """Converged SCF object: 'ROKS' / 'UKS' with the notebook's irrep_nelec,
-    'ROKS_AUFBAU' = example/spin up.ipynb (H 0 0 0; F 0 0 1.0, no constraint)."""
+    'ROKS_AUFBAU' = example/spin up.ipynb (H 0 0 0; F 0 0 1.0, no constraint);
+    'ROKS_TPSS' / 'UKS_TPSS': the same molecule with the TPSS meta-GGA (unpinned
+    energy; the source of the MGGA response checks)."""
+    if kind.endswith("_TPSS"):
+        mf = (ROKS if kind.startswith("ROKS") else UKS)(hf_mol(), "tpss")
+        mf.irrep_nelec = dict(HF_IRREP_NELEC)
+        mf.conv_tol = 1e-11
+        mf.kernel()
+        assert mf.converged
+        return mf
     if kind == "ROKS_AUFBAU":
         mol = M("H 0 0 0; F 0 0 1.0", basis="6-31G", spin=2, symmetry="C2v")
         mf = ROKS(mol, "bhandhlyp")
@@ -76,6 +85,7 @@ def fd_xc_response(scf, mfield, z, eps=1e-5):
     nov = [co.shape[1] * cv.shape[1] for co, cv in blocks]
     d0 = scf._dm
     out = np.empty_like(z)
+    # (MGGA: tau depends on D through 1/2 sum_c d_c phi D d_c phi, symmetric in D as well)
     for x in range(z.shape[0]):
         parts = [z[x, :nov[0]], z[x, nov[0]:]]
         d1 = np.array([np.einsum('ov,pv,qo->pq', parts[s].reshape(co.shape[1], cv.shape[1]), cv, co)

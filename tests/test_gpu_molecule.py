@@ -123,7 +123,7 @@ def test_rotatory_strengths_of_mirror_images(torch):
     assert np.abs(r1 + r2).max() <= 1e-4 * scale
 
 
-@pytest.mark.parametrize("kind", ["ROKS", "UKS"])
+@pytest.mark.parametrize("kind", ["ROKS", "UKS", "ROKS_TPSS", "UKS_TPSS"])
 def test_device_gga_xc_response_equals_fd_of_vxc(torch, kind):
     """The device's fused GGA XC contraction (forward U / W, point kernel, back L / M)
     against the finite-difference derivative of the SCF's V_xc (E_SCF pinned to the
@@ -133,7 +133,7 @@ def test_device_gga_xc_response_equals_fd_of_vxc(torch, kind):
     from xtddft_amd.operator import DeviceOperator
     from xtddft_amd.synthetic import make_trial_vectors
     scf, mf = hf_scf(kind), hf_meanfield(kind)
-    name = "XTDA" if kind == "ROKS" else "UTDA"
+    name = "XTDA" if kind.startswith("ROKS") else "UTDA"
     op1 = DeviceOperator(mf, name)
     op0 = DeviceOperator(dataclasses.replace(mf, fxc=mf.fxc * 0.0), name)
     z = make_trial_vectors(3, op1.dim)

@@ -65,7 +65,7 @@ def test_golden_fixtures(dev, case):
 
 @pytest.mark.parametrize("xct,omega,kind", [("GGA", 0.0, "RO"), ("LDA", 0.0, "RO"), ("HF", 0.0, "RO"),
                                             ("GGA", 0.33, "RO"), ("GGA", 0.0, "U"), ("LDA", 0.33, "U"),
-                                            ("HF", 0.0, "U")])
+                                            ("HF", 0.0, "U"), ("MGGA", 0.0, "RO"), ("MGGA", 0.0, "U")])
 @pytest.mark.parametrize("nz", [1, 7, 41])
 def test_xtda_utda(dev, xct, omega, kind, nz):
     mf = make_mf(nao=26, nc=5, no=2, xctype=xct, kind=kind, omega=omega,

@@ -125,3 +125,21 @@ def test_oracle_stored_eri_route_equals_df():
     z = make_trial_vectors(3, hdiag.size)
     ref = vind(z)
     assert np.abs(vind2(z) - ref).max() < 1e-12 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("nz", [1, 3])
+def test_mgga_vind_equals_explicit_a(nz):
+    """MGGA: the AO-route response (nr_uks_fxc restated with tau) and the explicit-A
+    kernel loop (XTDA.py:239-276 restated) are two reference code paths for the same
+    operator: equal to round-off on a synthetic ROKS problem."""
+    from oracle import xtda as ox
+    from xtddft_amd.synthetic import make_mf, make_trial_vectors
+    from xtddft_amd.utils import order_pyscf2my
+    mf = make_mf(nao=20, nc=4, no=2, ngrid=600, xctype="MGGA", hyb=0.2)
+    vind, hdiag = ox.gen_tda_operation(mf)
+    A = ox.full_diag_matrix(mf)
+    info = mf.shape_info()
+    order = order_pyscf2my(info['nc'], info['no'], info['nv'])
+    z = make_trial_vectors(nz, hdiag.size)
+    zm = z[:, order]
+    assert np.abs(vind(z)[:, order] - zm @ A.T).max() < 1e-13 * np.abs(A).max()

@@ -196,7 +196,7 @@ def test_chiral_mol():
     assert not chiral_mol(Geo([[1, 0, 0], [0, 0, 0], [0, 0, 1.5], [-1, 0, 1.5]], [1, 9, 9, 1]))  # trans
 
 
-@pytest.mark.parametrize("kind", ["ROKS", "UKS"])
+@pytest.mark.parametrize("kind", ["ROKS", "UKS", "ROKS_TPSS"])
 def test_oracle_gga_xc_response_equals_fd_of_vxc(kind):
     """The oracle's nr_uks_fxc restatement (GGA, hermi=0) equals the finite-difference
     derivative of the SCF's V_xc -- whose energy matches the reference's printed
@@ -386,3 +386,72 @@ def test_f_shell_host_integrals_consistent():
     q = (s / np.pi) ** 1.5 * (np.pi / (2 * s)) ** 0.75
     vnuc = -(mol._charges[0] * j3[0] + mol._charges[1] * j3[1]) * q
     assert np.abs(vnuc - mol.intor("int1e_nuc")).max() < 1e-9 * np.abs(vnuc).max()
+
+
+def test_tpss_exact_hydrogen_atom():
+    """TPSS meta-GGA (qc/xc.py) pinned by two exact constraints of the functional
+    (PRL 91, 146401): the hydrogen-atom exchange energy is -5/16 Ha and the
+    correlation energy of a one-electron density vanishes (revPKZB is
+    self-interaction free).  Exact density e^{-2r}/pi, Gauss-Laguerre radial
+    quadrature (error ~1e-7 from the density cutoff); derivatives finite."""
+    import torch
+    from scipy.special import roots_laguerre
+    from xtddft_amd.qc import xc
+    x, w = roots_laguerre(150)
+    r, wr = x / 2.0, w * np.exp(x) / 2.0
+    n = np.exp(-2 * r) / np.pi
+    keep = n > 1e-14
+    r, wr, n = r[keep], wr[keep], n[keep]
+    dn = -2.0 * n
+    tau = dn ** 2 / (8.0 * n)                  # one orbital: tau = tau_W
+    t = torch.tensor
+    ra, tiny = t(n), torch.full((n.size,), 1e-30, dtype=torch.float64)
+    z = torch.zeros_like(ra)
+    wq = 4 * np.pi * r ** 2 * wr
+    ex = xc._tpss_x(ra, tiny, t(dn ** 2), z, z, t(tau), tiny, torch).numpy()
+    ec = xc._tpss_c(ra, tiny, t(dn ** 2), z, z, t(tau), tiny, torch).numpy()
+    assert abs((wq * n).sum() - 1.0) < 1e-9
+    assert abs((wq * ex).sum() + 0.3125) < 2e-7
+    assert abs((wq * ec).sum()) < 1e-12
+    rho = np.zeros((2, 5, n.size))
+    rho[0, 0], rho[0, 3], rho[0, 4] = n, dn, tau
+    exc, vxc, fxc = xc.eval_xc_eff("TPSS", rho, deriv=2)
+    assert np.isfinite(vxc).all() and np.isfinite(fxc).all()
+
+
+def test_tpss_potential_is_the_energy_derivative():
+    """vxc of TPSS (autograd) against central differences of the energy density at
+    spin-polarised points with tau > tau_W (all five components, both spins)."""
+    from xtddft_amd.qc import xc
+    rng = np.random.default_rng(1)
+    G = 50
+    rho = np.zeros((2, 5, G))
+    for s in range(2):
+        rho[s, 0] = rng.uniform(0.01, 2, G)
+        rho[s, 1:4] = rng.normal(size=(3, G)) * 0.5 * rho[s, 0]
+        tw = (rho[s, 1:4] ** 2).sum(0) / (8 * rho[s, 0])
+        rho[s, 4] = tw * rng.uniform(1.05, 3, G) + 0.1 * rho[s, 0] ** (5 / 3)
+    exc, vxc, fxc = xc.eval_xc_eff("TPSS", rho, deriv=2)
+
+    def energy(rr):
+        return (xc.eval_xc_eff("TPSS", rr, deriv=1)[0] * (rr[0, 0] + rr[1, 0])).sum()
+    for s in range(2):
+        for c in range(5):
+            h = 1e-6 * max(1e-3, abs(rho[s, c, 7]))
+            rp, rm = rho.copy(), rho.copy()
+            rp[s, c, 7] += h
+            rm[s, c, 7] -= h
+            fd = (energy(rp) - energy(rm)) / (2 * h)
+            assert abs(fd - vxc[s, c, 7]) < 1e-6 * max(1.0, abs(vxc[s, c, 7]))
+    # fxc symmetric and equal to the derivative of vxc
+    assert np.abs(fxc - fxc.transpose(2, 3, 0, 1, 4)).max() < 1e-10 * np.abs(fxc).max()
+
+
+def test_tpss_roks_scf_converges():
+    """ROKS TPSS on the reference's HF molecule / 6-31G (irrep_nelec as the notebook):
+    the meta-GGA SCF (tau density and potential) converges; the energy is unpinned
+    offline (no libxc printout), its size checked against BHandHLYP's."""
+    from molecules import hf_scf, reference_outputs
+    mf = hf_scf("ROKS_TPSS")
+    assert mf.converged and mf.xctype == "MGGA"
+    assert abs(mf.e_tot - reference_outputs()["roks_bhandhlyp_e_tot"]) < 0.1

@@ -4,12 +4,16 @@
 //   hipcc --offload-arch=gfx950 -O3 tools/mfma_probe2.hip -o /tmp/mp2 && /tmp/mp2
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#pragma clang diagnostic ignored "-Wunused-result"
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+// MODE 0: MFMA only; 1: + 4 ds_read_b64 per step used in the same step; 2: 1 + 2 global
+// loads per step; 3: the 4 reads one step ahead; 4: 2 ds_read_b128 per step (same bytes);
+// 5: 1 + 12 VALU integer ops per step; 6: 1 + a uniform scalar branch per step
 template <int MODE>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
 probe(const double* __restrict__ g, double* out, int iters) {
-  __shared__ double sb[8192];
+  __shared__ __attribute__((aligned(16))) double sb[8192];
   const int tid = threadIdx.x;
   for (int i = tid; i < 8192; i += 512) sb[i] = 1e-3 * i;
   __syncthreads();
@@ -19,24 +23,50 @@ probe(const double* __restrict__ g, double* out, int iters) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[t][j] = (d4){0, 0, 0, 0};
   double a0 = 1e-3 * tid, a1 = 2e-3 * tid;
-  double b[4] = {1.0, 1.1, 1.2, 1.3};
+  double b[4] = {1.0, 1.1, 1.2, 1.3}, bn[4];
   const double* gp = g + (blockIdx.x * 512 + tid) % 65536;
+  int ctr = tid;
+  if (MODE == 3) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = sb[((tid + 16 * j) & 8191)];
+  }
   for (int it = 0; it < iters; ++it) {
-    if (MODE >= 1) {
+    if (MODE == 1 || MODE == 2 || MODE == 5 || MODE == 6) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[j] = sb[((it * 64 + tid + 16 * j) & 8191)];
     }
-    if (MODE >= 2) {
+    if (MODE == 3) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bn[j] = sb[(((it + 1) * 64 + tid + 16 * j) & 8191)];
+    }
+    if (MODE == 4) {
+      typedef double d2 __attribute__((ext_vector_type(2)));
+      const d2* p2 = (const d2*)sb;
+      const d2 u = p2[((it * 64 + tid) & 4095)], v = p2[((it * 64 + tid + 32) & 4095)];
+      b[0] = u[0]; b[1] = u[1]; b[2] = v[0]; b[3] = v[1];
+    }
+    if (MODE == 2) {
       a0 = gp[(it * 128) & 65535];
       a1 = gp[(it * 128 + 64) & 65535];
+    }
+    if (MODE == 5) {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) ctr = (ctr * 3 + k) ^ (ctr >> 2);
+    }
+    if (MODE == 6) {
+      if (__builtin_amdgcn_readfirstlane(it) % 7 == 3) a0 += 1e-9;
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(t ? a1 : a0, b[j], acc[t][j], 0, 0, 0);
+    if (MODE == 3) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = bn[j];
+    }
   }
-  double s = 0;
+  double s = ctr * 1e-30;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -53,12 +83,16 @@ int main() {
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   const int iters = 20000;
-  for (int blocks : {256, 512}) {
-    for (int mode = 0; mode < 3; ++mode) {
+  for (int blocks : {256}) {
+    for (int mode = 0; mode < 7; ++mode) {
       auto run = [&]() {
         if (mode == 0) probe<0><<<blocks, 512>>>(g, out, iters);
         if (mode == 1) probe<1><<<blocks, 512>>>(g, out, iters);
         if (mode == 2) probe<2><<<blocks, 512>>>(g, out, iters);
+        if (mode == 3) probe<3><<<blocks, 512>>>(g, out, iters);
+        if (mode == 4) probe<4><<<blocks, 512>>>(g, out, iters);
+        if (mode == 5) probe<5><<<blocks, 512>>>(g, out, iters);
+        if (mode == 6) probe<6><<<blocks, 512>>>(g, out, iters);
       };
       run();
       hipDeviceSynchronize();
@@ -69,8 +103,10 @@ int main() {
       float ms;
       hipEventElapsedTime(&ms, e0, e1);
       const double flops = 2.0 * 16 * 16 * 4 * 8.0 * iters * (blocks * 512 / 64);
-      printf("blocks %d mode %d (%s): %.1f TFLOP/s\n", blocks, mode,
-             mode == 0 ? "MFMA only" : mode == 1 ? "+4 LDS reads/step" : "+2 global loads/step", flops / ms / 1e9);
+      const char* what[7] = {"MFMA only", "+4 ds_read_b64/step", "+4 LDS +2 global loads/step",
+                             "+4 LDS reads one step ahead", "+2 ds_read_b128/step", "+4 LDS +12 VALU int/step",
+                             "+4 LDS + scalar branch/step"};
+      printf("blocks %d mode %d (%s): %.1f TFLOP/s\n", blocks, mode, what[mode], flops / ms / 1e9);
     }
   }
   return 0;

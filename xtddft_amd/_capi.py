@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "_lib", "libxtddft_amd.so")
 XT_PTR_HOST = 0
 XT_PTR_DEVICE = 1
 KIND = {"XTDA": 0, "UTDA": 1, "SF_DOWN": 2, "SF_UP": 3, "XSF": 4}
-XC = {"HF": 0, "LDA": 1, "GGA": 2}
+XC = {"HF": 0, "LDA": 1, "GGA": 2, "MGGA": 3}
 K_MODE = {"auto": 0, "direct": 1, "stored": 2}
 K_MODE_NAME = {v: k for k, v in K_MODE.items()}
 

@@ -63,7 +63,8 @@ struct xt_ctx {
   xt_desc d;
   hipStream_t st = nullptr;
   int nbasis = 1;            // MO bases: 1 restricted, 2 unrestricted
-  int ncomp = 1;
+  int ncomp = 1;                 // MO planes on the grid: value (+ 3 gradients for GGA / MGGA)
+  int nkc = 1;                   // kernel components: 1 LDA, 4 GGA, 5 MGGA (+ tau)
   int nchan = 2;             // spin channels in the trial vector
   int O = 0, V = 0, v0 = 0;  // superset occupied / virtual dims, vir MO offset
   int occ_basis[2] = {0, 0}, vir_basis[2] = {0, 0};
@@ -72,7 +73,7 @@ struct xt_ctx {
   bool has_vects = false;    // XSF OO basis set (empty for a doublet: no^2 - 1 = 0)
   DevBuf C, Bmo, Bmo_lr, Phi, kern, F, eps, vects;
   DevBuf ze, acc, kx, zr, tbuf, ubuf, gam, gam2, ws, stage, stage2, zin, sout, trace;
-  DevBuf zp, accT, wbuf;
+  DevBuf zp, accT, wbuf, taubuf;
   hipEvent_t ev[5];
   double timings[4] = {0, 0, 0, 0};
   // live per-kernel timing of tagged GEMM classes (bench roofline); mask bit t = tag t
@@ -202,15 +203,15 @@ int xt_create(const xt_desc* desc, xt_ctx** out) {
     return fail(XT_ERR_ARG, "XSF spin adaptation needs ROKS with no >= 2 (2S-1 > 0)");
   if (d.kind == XT_KIND_XSF && d.remove && d.no < 1)
     return fail(XT_ERR_ARG, "XSF OO compression needs an open shell");
-  if (d.xctype < XT_XC_NONE || d.xctype > XT_XC_GGA) return fail(XT_ERR_ARG, "bad xctype");
-  if ((d.kind == XT_KIND_SF_DOWN || d.kind == XT_KIND_SF_UP || d.kind == XT_KIND_XSF) && d.xctype == XT_XC_GGA)
-    ; // ALDA0 uses densities only; the grid needs ao[0] only (SF_TDA.py:73-80)
+  if (d.xctype < XT_XC_NONE || d.xctype > XT_XC_MGGA) return fail(XT_ERR_ARG, "bad xctype");
+  // (spin flip: ALDA0 uses densities only, the grid needs ao[0] only, SF_TDA.py:73-80)
   HIPCHK(hipSetDevice(d.device));
   xt_ctx* c = new xt_ctx();
   c->d = d;
   c->nbasis = d.restricted ? 1 : 2;
   const bool sf = (d.kind == XT_KIND_SF_DOWN || d.kind == XT_KIND_SF_UP || d.kind == XT_KIND_XSF);
-  c->ncomp = (d.xctype == XT_XC_GGA && !sf) ? 4 : 1;
+  c->ncomp = ((d.xctype == XT_XC_GGA || d.xctype == XT_XC_MGGA) && !sf) ? 4 : 1;
+  c->nkc = (d.xctype == XT_XC_MGGA && !sf) ? 5 : c->ncomp;
   const int nb = d.restricted ? 0 : 1;   // beta basis index
   if (d.kind == XT_KIND_XTDA || d.kind == XT_KIND_UTDA) {
     c->nchan = 2; c->O = d.nc + d.no; c->V = d.no + d.nv; c->v0 = d.nc;
@@ -252,7 +253,7 @@ int xt_destroy(xt_ctx* c) {
   (void)hipSetDevice(c->d.device);
   DevBuf* bufs[] = {&c->C, &c->Bmo, &c->Bmo_lr, &c->Phi, &c->kern, &c->F, &c->eps, &c->vects,
                     &c->ze, &c->acc, &c->kx, &c->zr, &c->tbuf, &c->ubuf, &c->gam, &c->gam2, &c->ws,
-                    &c->stage, &c->stage2, &c->zin, &c->sout, &c->trace, &c->zp, &c->accT, &c->wbuf,
+                    &c->stage, &c->stage2, &c->zin, &c->sout, &c->trace, &c->zp, &c->accT, &c->wbuf, &c->taubuf,
                     &c->Kx};
   for (DevBuf* b : bufs) b->release();
   for (int i = 0; i < 5; ++i) (void)hipEventDestroy(c->ev[i]);
@@ -518,7 +519,7 @@ int xt_set_grid(xt_ctx* c, const double* ao, const double* w, const double* kern
   if (sf) {
     RET(to_device(c, c->kern, kernel, (size_t)ng, ptr_kind));   // already weighted
   } else {
-    const size_t n4 = (size_t)4 * ncomp * ncomp;
+    const size_t n4 = (size_t)4 * c->nkc * c->nkc;
     RET(to_device(c, c->kern, kernel, n4 * ng, ptr_kind));
     RET(c->stage2.ensure(ng));
     const hipMemcpyKind k = ptr_kind == XT_PTR_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
@@ -964,15 +965,19 @@ static int xc_response(xt_ctx* c, int nz) {
   const int O = c->O, V = c->V, nmo = c->d.nmo, ng = c->d.ngrid, nc = c->ncomp;
   const int nch = c->nchan;
   const bool gga = (nc == 4);
+  const bool mgga = (c->nkc == 5);
   const long chs = (long)nz * O * V;
   Group gr[2];
   const int ngr = channel_groups(c, gr);
-  const size_t per_g = (size_t)nch * nz * O + (gga ? (size_t)nch * nz * 3 : 0);
+  const size_t per_g = (size_t)nch * nz * O * (mgga ? 4 : 1) + (gga ? (size_t)nch * nz * 3 : 0);
   size_t G = ((size_t)8 << 30) / (8 * per_g);
   if (G > (size_t)ng) G = ng;
   if (G < 64) G = 64 < (size_t)ng ? 64 : ng;
   RET(c->ubuf.ensure((size_t)nch * nz * O * G));
   if (gga) RET(c->wbuf.ensure((size_t)nch * nz * 3 * (G + XC_GRID_SLACK)));
+  // MGGA: three tau planes T_c = dPhiV_c Ze^T laid out like U (forward), then the tau
+  // potential's back operands 1/2 wv_tau dPhiO_c (point kernel)
+  if (mgga) RET(c->taubuf.ensure((size_t)3 * nch * nz * O * G));
   const long compP = (long)ng * nmo;
   const long basP = (long)nc * compP;
   const int nab = (V + 15) / 16;
@@ -992,6 +997,15 @@ static int xc_response(xt_ctx* c, int nz) {
       f1.C = Ug[q]; f1.ldc = ldU[q];
       f1.tag = 2;
       RET(gemm(c, f1));
+      if (mgga) {
+        const long tcs = (long)nch * nz * O * n;
+        for (int cc = 1; cc < 4; ++cc) {   // T_c[g][(x,i)] = sum_a dPhiV_c[g][a] Ze[(x,i)][a]
+          GemmDesc ft = f1;
+          ft.A = PV + cc * compP;
+          ft.C = c->taubuf.p + (cc - 1) * tcs + (long)gr[q].ch0 * nz * O * n;
+          RET(gemm(c, ft));
+        }
+      }
       // the dedicated kernel pays off from ~6 occupied 16-row blocks up (O = 101: 168.6 vs
       // 173.1 ms/step; O = 34 / 37: 18 % / 15 % slower than the engine's mode 1)
       const bool w_ded = c->w_kernel == 1 || (c->w_kernel == 2 && O >= 96);
@@ -1030,9 +1044,17 @@ static int xc_response(xt_ctx* c, int nz) {
         Us[s] = Ug[q] + (long)off * nz * O; lus[s] = ldU[q];
         Rs[s] = gga ? Rg[q] + (long)off * nz * 3 : nullptr; lrs[s] = ldR[q];
       }
-      xc_uks_w(c->st, nc, n, g0, ng, nz, O, nmo, compP,
-               c->Phi.p + c->occ_basis[0] * basP, c->Phi.p + c->occ_basis[1] * basP,
-               c->kern.p, Us[0], lus[0], Us[1], lus[1], Rs[0], lrs[0], Rs[1], lrs[1]);
+      if (mgga) {
+        double* Ts[2];
+        for (int s = 0; s < 2; ++s) Ts[s] = c->taubuf.p + (Us[s] - c->ubuf.p);   // same layout as U
+        xc_uks_mgga(c->st, n, g0, ng, nz, O, nmo, compP, c->Phi.p + c->occ_basis[0] * basP,
+                    c->Phi.p + c->occ_basis[1] * basP, c->kern.p, Us[0], lus[0], Us[1], lus[1], Ts[0], Ts[1],
+                    (long)nch * nz * O * n, Rs[0], lrs[0], Rs[1], lrs[1]);
+      } else {
+        xc_uks_w(c->st, nc, n, g0, ng, nz, O, nmo, compP,
+                 c->Phi.p + c->occ_basis[0] * basP, c->Phi.p + c->occ_basis[1] * basP,
+                 c->kern.p, Us[0], lus[0], Us[1], lus[1], Rs[0], lrs[0], Rs[1], lrs[1]);
+      }
     } else {
       xc_sf(c->st, n, g0, nz, O, nmo, c->Phi.p + c->occ_basis[0] * basP, c->kern.p, Ug[0]);
     }
@@ -1047,6 +1069,15 @@ static int xc_response(xt_ctx* c, int nz) {
       b1.C = c->acc.p + gr[q].ch0 * chs; b1.ldc = V; b1.beta = 1.0;
       b1.tag = 3;
       RET(gemm(c, b1));
+      if (mgga) {
+        const long tcs = (long)nch * nz * O * n;
+        for (int cc = 1; cc < 4; ++cc) {   // acc[(x,i)][a] += sum_g (1/2 wv_tau dPhiO_c)[g][(x,i)] dPhiV_c[g][a]
+          GemmDesc bt = b1;
+          bt.A = c->taubuf.p + (cc - 1) * tcs + (long)gr[q].ch0 * nz * O * n;
+          bt.B = PV + cc * compP;
+          RET(gemm(c, bt));
+        }
+      }
       if (gga) {
         if (O <= 128 && c->m_kernel) {
           // dedicated kernel (xt_xcm.hip); tag 5 timing around it and its reduce

@@ -806,6 +806,115 @@ void xc_uks(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, 
   else
     hipLaunchKernelGGL(k_xc_uks<1>, dim3(blocks), dim3(256), 0, st, G, g0, ngrid, nz, O, nmo, phi0, phi1, wfxc, U);
 }
+// Meta-GGA point kernel (nr_uks_fxc's MGGA branch, XTDA.py:514; explicit form
+// XTDA.py:239-276): the GGA contraction above plus the kinetic-energy density,
+//   tau1[s] = 1/2 sum_c sum_i dPhiO_c[i] T_s[c][x][i],  T_s[c] = dPhiV_c Ze^T (GEMMs),
+// the 5 x 5 (rho, grad rho, tau) kernel block, and the tau potential's back operands
+//   T_s[c][x][i] <- 1/2 wv[s][4] dPhiO_c[i]       (sigma += T_c^T dPhiV_c, GEMMs).
+// One block per grid point, one wave per trial vector x (both spins); correctness
+// first (the MGGA classes are plain GEMMs around it).
+__global__ void __launch_bounds__(256)
+k_xc_uks_mgga(int g0, int ngrid, int nz, int O, int nmo, long compP,
+              const double* __restrict__ pO0, const double* __restrict__ pO1,
+              const double* __restrict__ wfxc,
+              double* __restrict__ U0, long ldU0, double* __restrict__ U1, long ldU1,
+              double* __restrict__ T0, double* __restrict__ T1, long tcs,
+              double* __restrict__ R0, long ldR0, double* __restrict__ R1, long ldR1) {
+  constexpr int NC = 4, NK = 5;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  __shared__ double sk[4 * NK * NK];   // sk[((t*NK + y')*2 + s)*NK + y] = (w fxc) at this point
+  const int g = blockIdx.x;
+  const long gg = g0 + g;
+  const bool same = (pO0 == pO1);
+  const double* so[2];
+  so[0] = sm;
+  so[1] = same ? so[0] : sm + NC * O;
+  for (int s = 0; s < (same ? 1 : 2); ++s) {
+    const double* po = s ? pO1 : pO0;
+    double* dso = sm + s * NC * O;
+    for (int k = threadIdx.x; k < NC * O; k += blockDim.x) {
+      const int cc = k / O, i = k % O;
+      dso[k] = po[cc * compP + gg * nmo + i];
+    }
+  }
+  for (int k = threadIdx.x; k < 4 * NK * NK; k += blockDim.x) sk[k] = wfxc[(long)k * ngrid + gg];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nwave = blockDim.x >> 6;
+  double* Ub[2] = {U0 + g * ldU0, U1 + g * ldU1};
+  double* Tb[2] = {T0 + g * ldU0, T1 + g * ldU1};
+  double* Rb[2] = {R0 + g * ldR0, R1 + g * ldR1};
+  for (int x = wave; x < nz; x += nwave) {
+    double acc[2][NK];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int c = 0; c < NK; ++c) acc[s][c] = 0.0;
+    for (int i = lane; i < O; i += 64) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const double u = Ub[s][(long)x * O + i];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[s][c] += u * so[s][c * O + i];
+#pragma unroll
+        for (int c = 1; c < NC; ++c) acc[s][4] += Tb[s][(c - 1) * tcs + (long)x * O + i] * so[s][c * O + i];
+      }
+    }
+    double rho[2][NK];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int c = 0; c < NK; ++c) {
+        double v = acc[s][c];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (c >= 1 && c <= 3) v += Rb[s][3 * x + c - 1];
+        rho[s][c] = c == 4 ? 0.5 * v : v;
+      }
+    double wv[2][NK];
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int y = 0; y < NK; ++y) {
+        double v = 0.0;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int yy = 0; yy < NK; ++yy) v += sk[((t * NK + yy) * 2 + s) * NK + y] * rho[t][yy];
+        wv[s][y] = v;
+      }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      for (int i = lane; i < O; i += 64) {
+        double l = 0.0;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) l += wv[s][c] * so[s][c * O + i];
+        Ub[s][(long)x * O + i] = l;
+#pragma unroll
+        for (int c = 1; c < NC; ++c) Tb[s][(c - 1) * tcs + (long)x * O + i] = 0.5 * wv[s][4] * so[s][c * O + i];
+      }
+    }
+    if (lane < 6) {   // all reads of R for this x are done (shuffle-synchronised wave)
+      const int s = lane / 3, c = lane % 3 + 1;
+      double v = 0.0;
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int y = 1; y < NC; ++y)
+          if (ss == s && y == c) v = wv[ss][y];
+      Rb[s][3 * x + c - 1] = v;
+    }
+  }
+}
+void xc_uks_mgga(hipStream_t st, int G, int g0, int ngrid, int nz, int O, int nmo, long compP, const double* pO0,
+                 const double* pO1, const double* wfxc, double* U0, long ldU0, double* U1, long ldU1, double* T0,
+                 double* T1, long tcs, double* R0, long ldR0, double* R1, long ldR1) {
+  const bool same = (pO0 == pO1);
+  const size_t lds = (same ? 1 : 2) * (size_t)4 * O * sizeof(double);
+  hipLaunchKernelGGL(k_xc_uks_mgga, dim3(G), dim3(256), lds, st, g0, ngrid, nz, O, nmo, compP, pO0, pO1, wfxc, U0,
+                     ldU0, U1, ldU1, T0, T1, tcs, R0, ldR0, R1, ldR1);
+}
 void xc_uks_w(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
               const double* pO0, const double* pO1, const double* wfxc, double* U0, long ldU0,
               double* U1, long ldU1, double* R0, long ldR0, double* R1, long ldR1) {

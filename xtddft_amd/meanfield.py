@@ -78,10 +78,11 @@ class MeanField:
                long-range operator; ``chol_tol`` the device Cholesky
                tolerance (0: 1e-13 x largest diagonal).
     fxc      : (2, ncomp, 2, ncomp, ngrid) un-weighted UKS second derivative
-               kernel (``cache_xc_kernel`` output, XTDA.py:504).
+               kernel (``cache_xc_kernel`` output, XTDA.py:504); ncomp 1 / 4 / 5
+               for LDA / GGA / MGGA (rho, grad rho, tau -- PySCF's MGGA layout).
     fxc_sf   : (ngrid,) ALDA0 spin-flip kernel already multiplied by the grid
                weight (``cache_xc_kernel_sf``, SF_TDA.py:82-84).
-    xctype   : 'HF' | 'LDA' | 'GGA'
+    xctype   : 'HF' | 'LDA' | 'GGA' | 'MGGA'
     omega, alpha, hyb : ``ni.rsh_and_hybrid_coeff`` (XTDA.py:501).
     """
     mol: Mole
@@ -113,7 +114,7 @@ class MeanField:
         self.mo_coeff = np.asarray(self.mo_coeff, dtype=np.float64)
         self.mo_occ = np.asarray(self.mo_occ)
         self.mo_energy = np.asarray(self.mo_energy, dtype=np.float64)
-        if self.xctype not in ("HF", "LDA", "GGA"):
+        if self.xctype not in ("HF", "LDA", "GGA", "MGGA"):
             raise ValueError(f"unsupported xctype {self.xctype!r}")
         if self.is_rohf:
             occ = self.mo_occ

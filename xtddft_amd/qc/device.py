@@ -108,12 +108,14 @@ class DeviceEngine:
 
     # ------------------------------------------------------------ XC
     def _rho(self, dm):
-        """(ncomp, G) density and gradient of a symmetric density matrix."""
+        """(ncomp, G) density and gradient (MGGA: + tau) of a symmetric density matrix."""
         ao = self.ao
         c0 = self._mm(ao[0], dm)
         rho = [(ao[0] * c0).sum(1)]
         for k in range(1, ao.shape[0]):
             rho.append(2.0 * (ao[k] * c0).sum(1))
+        if self.xctype == "MGGA":
+            rho.append(0.5 * sum((ao[k] * self._mm(ao[k], dm)).sum(1) for k in range(1, 4)))
         return self.torch.stack(rho)
 
     def rho(self, dms):
@@ -131,12 +133,16 @@ class DeviceEngine:
         vm = []
         for s in range(2):
             wv = vxc[s] * self.w
-            if self.xctype == "GGA":
+            if self.xctype in ("GGA", "MGGA"):
                 wv = wv.clone()
                 wv[0] *= 0.5
-                aow = (wv[:, :, None] * ao).sum(0)
+                aow = (wv[:4, :, None] * ao[:4]).sum(0)
                 v = self._mm(ao[0], aow, ta=1)
-                vm.append(v + v.T)
+                v = v + v.T
+                if self.xctype == "MGGA":     # tau part: 1/2 sum_c grad_c phi^T w_tau grad_c phi
+                    for k in range(1, 4):
+                        v = v + 0.5 * self._mm(ao[k], (wv[4][:, None] * ao[k]).contiguous(), ta=1)
+                vm.append(v)
             else:
                 vm.append(self._mm(ao[0], (wv[0][:, None] * ao[0]).contiguous(), ta=1))
         return e, torch.stack(vm).cpu().numpy()

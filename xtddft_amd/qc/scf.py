@@ -129,7 +129,8 @@ class _SCFBase:
                 self.grids = gen_grids(mol)
             self.timings["grid_s"] = time.perf_counter() - t0
             t0 = time.perf_counter()
-            self.ao = mol.eval_ao(self.grids.coords, deriv=1 if self.xctype == "GGA" else 0, device=dev)
+            self.ao = mol.eval_ao(self.grids.coords, deriv=1 if self.xctype in ("GGA", "MGGA") else 0,
+                                  device=dev)
             if self.ao.ndim == 2:
                 self.ao = self.ao[None]
             if dev is not None:
@@ -176,13 +177,17 @@ class _SCFBase:
         return vj, vk
 
     def _rho(self, dm):
-        """rho (4, ngrid) (or (1, ngrid)) of a symmetric density matrix."""
+        """rho (4, ngrid) (or (1, ngrid); MGGA (5, ngrid) with tau = 1/2 sum_c
+        grad_c phi D grad_c phi) of a symmetric density matrix."""
         ao = self.ao
         c0 = ao[0] @ dm
-        rho = np.empty((ao.shape[0], ao.shape[1]))
+        nc = 5 if self.xctype == "MGGA" else ao.shape[0]
+        rho = np.empty((nc, ao.shape[1]))
         rho[0] = np.einsum('gp,gp->g', ao[0], c0)
         for k in range(1, ao.shape[0]):
             rho[k] = 2.0 * np.einsum('gp,gp->g', ao[k], c0)
+        if nc == 5:
+            rho[4] = 0.5 * sum(np.einsum('gp,gp->g', ao[k], ao[k] @ dm) for k in range(1, 4))
         return rho
 
     def _vxc(self, dms):
@@ -204,11 +209,14 @@ class _SCFBase:
             exc_tot += float(np.sum(w * exc * (rho[0, 0] + rho[1, 0])))
             for s in range(2):
                 wv = vxc[s] * w
-                if self.xctype == "GGA":
+                if self.xctype in ("GGA", "MGGA"):
                     wv[0] *= 0.5
-                    aow = np.einsum('yg,ygp->gp', wv, ao)
+                    aow = np.einsum('yg,ygp->gp', wv[:4], ao[:4])
                     v = ao[0].T @ aow
                     vmat[s] += v + v.T
+                    if self.xctype == "MGGA":    # tau part: 1/2 sum_c grad_c phi^T w_tau grad_c phi
+                        for k in range(1, 4):
+                            vmat[s] += 0.5 * ao[k].T @ (wv[4][:, None] * ao[k])
                 else:
                     vmat[s] += ao[0].T @ (wv[0][:, None] * ao[0])
         return exc_tot, vmat

@@ -21,6 +21,19 @@ to round-off, no finite differences).  Forms follow libxc 7.0's definitions:
                     and VWN_RPA (libxc LDA_C_VWN_RPA: the RPA fits interpolated by
                     f(z) alone, e = e_P (1 - f(z)) + e_F f(z)).
 
+Meta-GGA (the reference's MGGA branches, XTDA.py:239-276 and nr_uks_fxc, XTDA.py:514):
+inputs (rho_s, grad rho_s, tau_s) per spin, PySCF's 5-component layout (2, 5, ngrid)
+with tau = 1/2 sum |grad phi|^2 (no Laplacian):
+
+* TPSS exchange     Tao, Perdew, Staroverov, Scuseria, PRL 91, 146401 (2003), eqs. 4-10,
+                    spin scaling E_x[n_a, n_b] = (E_x[2 n_a] + E_x[2 n_b]) / 2
+* TPSS correlation  revPKZB (eqs. 11-14) on PBE correlation (PRL 77, 3865 (1996)) over
+                    PW92 (libxc's PW_MOD parameters), d = 2.8 Ha^-1
+
+TPSS = TPSS x + TPSS c, TPSSh = 0.1 HF + 0.9 TPSS x + TPSS c.  Pinned by two exact
+properties of the functional (tests/test_qc.py): the hydrogen-atom exchange energy is
+exactly -5/16 Ha and the correlation energy of any one-electron density is zero.
+
 Hybrids: BHandHLYP = 0.5 HF + 0.5 B88 + LYP (libxc HYB_GGA_XC_BHANDHLYP), the
 reference's functional in every stored example (``example/XSF_TDA.ipynb``,
 ``spin up.ipynb``); B3LYP = 0.2 HF + 0.08 Slater + 0.72 B88 + 0.19 VWN_RPA +
@@ -52,7 +65,10 @@ _FUNCTIONALS = {
     "B3LYP": ([("slater", 0.08), ("b88", 0.72), ("vwn_rpa", 0.19), ("lyp", 0.81)], 0.2, "GGA"),
     "B3LYPG": ([("slater", 0.08), ("b88", 0.72), ("vwn_rpa", 0.19), ("lyp", 0.81)], 0.2, "GGA"),
     "B3LYP5": ([("slater", 0.08), ("b88", 0.72), ("vwn5", 0.19), ("lyp", 0.81)], 0.2, "GGA"),
+    "TPSS": ([("tpss_x", 1.0), ("tpss_c", 1.0)], 0.0, "MGGA"),
+    "TPSSH": ([("tpss_x", 0.9), ("tpss_c", 1.0)], 0.1, "MGGA"),
 }
+NCOMP = {"HF": 1, "LDA": 1, "GGA": 4, "MGGA": 5}
 
 
 def parse_xc(xc: str):
@@ -160,14 +176,112 @@ def _vwn_rpa(ra, rb, saa, sab, sbb, torch):
     return rho * (ep * (1.0 - fz) + ef * fz)
 
 
+# ---------------------------------------------------------------- TPSS (meta-GGA)
+_ZETA_MAX = 1.0 - 1e-10          # |zeta| cap (libxc's zeta threshold): (1 -+ zeta)^(-4/3) stays finite
+_TAU_MIN = 1e-30
+
+
+def _tpss_x_unpol(n, sigma, tau, torch):
+    """TPSS exchange energy density of a spin-unpolarised density n (PRL 91, 146401)."""
+    kappa, b, c, e, mu = 0.804, 0.40, 1.59096, 1.537, 0.21951
+    kf2 = (3.0 * math.pi ** 2 * n) ** (2.0 / 3.0)
+    p = sigma / (4.0 * kf2 * n * n)
+    tauw = sigma / (8.0 * n)
+    z = torch.clamp(tauw / torch.clamp(tau, min=_TAU_MIN), max=1.0)
+    alpha = (5.0 / 3.0) * p * (1.0 / torch.clamp(z, min=1e-300) - 1.0)
+    qb = 0.45 * (alpha - 1.0) / torch.sqrt(1.0 + b * alpha * (alpha - 1.0)) + 2.0 * p / 3.0
+    se = math.sqrt(e)
+    num = ((10.0 / 81.0 + c * z * z / (1.0 + z * z) ** 2) * p + 146.0 / 2025.0 * qb * qb
+           - 73.0 / 405.0 * qb * torch.sqrt(0.5 * (0.6 * z) ** 2 + 0.5 * p * p + 1e-40)
+           + (10.0 / 81.0) ** 2 * p * p / kappa + 2.0 * se * (10.0 / 81.0) * (0.6 * z) ** 2 + e * mu * p ** 3)
+    x = num / (1.0 + se * p) ** 2
+    fx = 1.0 + kappa - kappa / (1.0 + x / kappa)
+    return -0.75 * (3.0 / math.pi) ** (1.0 / 3.0) * n ** (4.0 / 3.0) * fx
+
+
+def _tpss_x(ra, rb, saa, sab, sbb, ta, tb, torch):
+    return 0.5 * (_tpss_x_unpol(2.0 * ra, 4.0 * saa, 2.0 * ta, torch)
+                  + _tpss_x_unpol(2.0 * rb, 4.0 * sbb, 2.0 * tb, torch))
+
+
+# PW92 with libxc's PW_MOD parameters: (A, alpha1, beta1..beta4) for ec(rs, 0), ec(rs, 1), -alpha_c
+_PW92 = ((0.0310907, 0.21370, 7.5957, 3.5876, 1.6382, 0.49294),
+         (0.01554535, 0.20548, 14.1189, 6.1977, 3.3662, 0.62517),
+         (0.0168869, 0.11125, 10.357, 3.6231, 0.88026, 0.49671))
+_FZ20 = 1.709920934161365617563962776245
+
+
+def _pw92_g(rs, prm, torch):
+    A, a1, b1, b2, b3, b4 = prm
+    srs = torch.sqrt(rs)
+    den = 2.0 * A * (b1 * srs + b2 * rs + b3 * rs * srs + b4 * rs * rs)
+    return -2.0 * A * (1.0 + a1 * rs) * torch.log1p(1.0 / den)
+
+
+def _ec_pw92(n, zeta, torch):
+    """PW92 correlation energy per particle."""
+    rs = (3.0 / (4.0 * math.pi * n)) ** (1.0 / 3.0)
+    ec0, ec1, mac = (_pw92_g(rs, prm, torch) for prm in _PW92)
+    fz = ((1.0 + zeta) ** (4.0 / 3.0) + (1.0 - zeta) ** (4.0 / 3.0) - 2.0) / (2.0 ** (4.0 / 3.0) - 2.0)
+    z4 = zeta ** 4
+    return ec0 - mac * fz * (1.0 - z4) / _FZ20 + (ec1 - ec0) * fz * z4
+
+
+def _ec_pbe(n, zeta, sigma, torch):
+    """PBE correlation energy per particle (PW92 + H)."""
+    beta, gamma = 0.06672455060314922, (1.0 - math.log(2.0)) / math.pi ** 2
+    ec = _ec_pw92(n, zeta, torch)
+    phi = 0.5 * ((1.0 + zeta) ** (2.0 / 3.0) + (1.0 - zeta) ** (2.0 / 3.0))
+    kf = (3.0 * math.pi ** 2 * n) ** (1.0 / 3.0)
+    ks2 = 4.0 * kf / math.pi
+    t2 = sigma / (4.0 * phi * phi * ks2 * n * n)
+    phi3 = phi ** 3
+    A = beta / gamma / torch.expm1(-ec / (gamma * phi3))
+    at2 = A * t2
+    return ec + gamma * phi3 * torch.log1p(beta / gamma * t2 * (1.0 + at2) / (1.0 + at2 + at2 * at2))
+
+
+def _tpss_c(ra, rb, saa, sab, sbb, ta, tb, torch):
+    n = ra + rb
+    zeta = torch.clamp((ra - rb) / n, -_ZETA_MAX, _ZETA_MAX)
+    stot = saa + 2.0 * sab + sbb
+    e_pbe = _ec_pbe(n, zeta, stot, torch)
+    one = torch.full_like(n, _ZETA_MAX)
+    e_a = torch.maximum(_ec_pbe(ra, one, saa, torch), e_pbe)       # fully polarised n_s alone
+    e_b = torch.maximum(_ec_pbe(rb, one, sbb, torch), e_pbe)
+    # xi = |grad zeta| / (2 (3 pi^2 n)^(1/3)), |grad zeta|^2 = 4 (rb^2 saa - 2 ra rb sab + ra^2 sbb) / n^4
+    gz2 = 4.0 * torch.clamp(rb * rb * saa - 2.0 * ra * rb * sab + ra * ra * sbb, min=0.0) / n ** 4
+    xi2 = gz2 / (4.0 * (3.0 * math.pi ** 2 * n) ** (2.0 / 3.0))
+    z2 = zeta * zeta
+    cnum = 0.53 + 0.87 * z2 + 0.50 * z2 * z2 + 2.26 * z2 ** 3
+    cden = (1.0 + 0.5 * xi2 * ((1.0 + zeta) ** (-4.0 / 3.0) + (1.0 - zeta) ** (-4.0 / 3.0))) ** 4
+    cc = cnum / cden
+    tauw = stot / (8.0 * n)
+    z = torch.clamp(tauw / torch.clamp(ta + tb, min=_TAU_MIN), max=1.0)
+    zz = z * z
+    e_rev = e_pbe * (1.0 + cc * zz) - (1.0 + cc) * zz * (ra / n * e_a + rb / n * e_b)
+    return n * e_rev * (1.0 + 2.8 * e_rev * zz * z)
+
+
 _PIECES = {"slater": _slater, "b88": _b88, "lyp": _lyp, "vwn5": _vwn5, "vwn_rpa": _vwn_rpa}
+_MPIECES = {"tpss_x": _tpss_x, "tpss_c": _tpss_c}
+
+
+def _energy_density(comps, ra, rb, saa, sab, sbb, ta, tb, torch):
+    eps = 0.0
+    for name, coef in comps:
+        if name in _MPIECES:
+            eps = eps + coef * _MPIECES[name](ra, rb, saa, sab, sbb, ta, tb, torch)
+        else:
+            eps = eps + coef * _PIECES[name](ra, rb, saa, sab, sbb, torch)
+    return eps
 
 
 def eval_xc_eff(xc: str, rho: np.ndarray, deriv: int = 1):
     """Spin-polarised XC on a grid.
 
-    rho : (2, 4, ngrid) for GGA (rho, d/dx, d/dy, d/dz per spin) or (2, ngrid) /
-          (2, 1, ngrid) for LDA.
+    rho : (2, 4, ngrid) for GGA (rho, d/dx, d/dy, d/dz per spin), (2, 5, ngrid) for
+          MGGA (+ tau), or (2, ngrid) / (2, 1, ngrid) for LDA.
     Returns (exc, vxc, fxc): exc (ngrid,) energy per particle, vxc (2, ncomp, ngrid),
     fxc (2, ncomp, 2, ncomp, ngrid) or None when deriv < 2.
     """
@@ -185,7 +299,7 @@ def _eval_xc_eff(torch, xc, rho, deriv):
     rho = np.asarray(rho, dtype=np.float64)
     if rho.ndim == 2:
         rho = rho[:, None, :]
-    ncomp = 4 if xctype == "GGA" else 1
+    ncomp = NCOMP[xctype]
     ng = rho.shape[-1]
     exc = np.zeros(ng)
     vxc = np.zeros((2, ncomp, ng))
@@ -201,16 +315,15 @@ def _eval_xc_eff(torch, xc, rho, deriv):
     rs = x.reshape(2, ncomp, -1)
     ra = torch.clamp(rs[0, 0], min=1e-30)
     rb = torch.clamp(rs[1, 0], min=1e-30)
-    if ncomp == 4:
-        ga, gb = rs[0, 1:], rs[1, 1:]
+    if ncomp >= 4:
+        ga, gb = rs[0, 1:4], rs[1, 1:4]
         saa = (ga * ga).sum(0)
         sab = (ga * gb).sum(0)
         sbb = (gb * gb).sum(0)
     else:
         saa = sab = sbb = torch.zeros_like(ra)
-    eps = 0.0
-    for name, coef in comps:
-        eps = eps + coef * _PIECES[name](ra, rb, saa, sab, sbb, torch)
+    ta, tb = (rs[0, 4], rs[1, 4]) if ncomp == 5 else (None, None)
+    eps = _energy_density(comps, ra, rb, saa, sab, sbb, ta, tb, torch)
     g = torch.autograd.grad(eps.sum(), x, create_graph=deriv >= 2)[0]
     exc[mask] = (eps / (ra + rb)).detach().numpy()
     vxc[:, :, mask] = g.detach().numpy().reshape(2, ncomp, -1)
@@ -221,7 +334,22 @@ def _eval_xc_eff(torch, xc, rho, deriv):
             H[k] = torch.autograd.grad(g[k].sum(), x, retain_graph=k < n - 1)[0].numpy()
         H = 0.5 * (H + H.transpose(1, 0, 2))       # exact symmetry (autograd round-off)
         fxc[..., mask] = H.reshape(2, ncomp, 2, ncomp, -1)
+    _screen_spin(rho, vxc, fxc, np)
     return exc, vxc, fxc
+
+
+def _screen_spin(rho, vxc, fxc, xp):
+    """A spin channel without density at a point (below DENS_THRESHOLD) carries no
+    potential or kernel there (libxc's per-spin screening; TPSS correlation's
+    fully polarised terms are singular in a vanishing channel)."""
+    for s in range(2):
+        off = rho[s, 0] < DENS_THRESHOLD
+        if not bool(off.any()):
+            continue
+        vxc[s, :, off] = 0.0
+        if fxc is not None:
+            fxc[s, :, :, :, off] = 0.0
+            fxc[:, :, s, :, off] = 0.0
 
 
 def eval_xc_eff_torch(xc: str, rho, deriv: int = 1):
@@ -231,7 +359,7 @@ def eval_xc_eff_torch(xc: str, rho, deriv: int = 1):
     with the same density screening and derivative layout."""
     import torch
     comps, _, xctype = parse_xc(xc)
-    ncomp = 4 if xctype == "GGA" else 1
+    ncomp = NCOMP[xctype]
     if rho.dim() == 2:
         rho = rho[:, None, :]
     rho = rho[:, :ncomp].to(torch.float64)
@@ -250,14 +378,13 @@ def eval_xc_eff_torch(xc: str, rho, deriv: int = 1):
     rs = x.reshape(2, ncomp, -1)
     ra = torch.clamp(rs[0, 0], min=1e-30)
     rb = torch.clamp(rs[1, 0], min=1e-30)
-    if ncomp == 4:
-        ga, gb = rs[0, 1:], rs[1, 1:]
+    if ncomp >= 4:
+        ga, gb = rs[0, 1:4], rs[1, 1:4]
         saa, sab, sbb = (ga * ga).sum(0), (ga * gb).sum(0), (gb * gb).sum(0)
     else:
         saa = sab = sbb = torch.zeros_like(ra)
-    eps = 0.0
-    for name, coef in comps:
-        eps = eps + coef * _PIECES[name](ra, rb, saa, sab, sbb, torch)
+    ta, tb = (rs[0, 4], rs[1, 4]) if ncomp == 5 else (None, None)
+    eps = _energy_density(comps, ra, rb, saa, sab, sbb, ta, tb, torch)
     g = torch.autograd.grad(eps.sum(), x, create_graph=deriv >= 2)[0]
     exc[idx] = (eps / (ra + rb)).detach()
     vxc[:, :, idx] = g.detach().reshape(2, ncomp, -1)
@@ -268,4 +395,5 @@ def eval_xc_eff_torch(xc: str, rho, deriv: int = 1):
             H[k] = torch.autograd.grad(g[k].sum(), x, retain_graph=k < n - 1)[0]
         H = 0.5 * (H + H.transpose(0, 1))
         fxc[..., idx] = H.reshape(2, ncomp, 2, ncomp, -1)
+    _screen_spin(rho, vxc, fxc, torch)
     return exc, vxc, fxc

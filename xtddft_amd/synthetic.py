@@ -98,7 +98,7 @@ def make_mf(nao=24, nc=5, no=2, naux=None, ngrid=None, xctype="GGA", hyb=0.2,
         raise ValueError("need at least one core and one virtual orbital")
     naux = naux if naux is not None else 3 * nao
     ngrid = ngrid if ngrid is not None else 60 * nao
-    ncomp = 4 if xctype == "GGA" else 1
+    ncomp = 4 if xctype in ("GGA", "MGGA") else 1     # AO values (+ gradients) on the grid
 
     eps_c = np.sort(rng.uniform(-1.0, -0.5, nc))
     eps_o = np.sort(rng.uniform(-0.45, -0.25, no))
@@ -155,7 +155,7 @@ def make_mf(nao=24, nc=5, no=2, naux=None, ngrid=None, xctype="GGA", hyb=0.2,
     grids = fxc = fxc_sf = None
     if xctype != "HF":
         grids = make_grid(rng, nao, ngrid, ncomp, grid_scale(ngrid, nocc, nvir, xc_target))
-        fxc = make_fxc(rng, ngrid, ncomp)
+        fxc = make_fxc(rng, ngrid, 5 if xctype == "MGGA" else ncomp)
         fxc_sf = -rng.uniform(0.1, 1.0, ngrid) * grids.weights
     else:
         hyb, alpha, omega = 1.0, 0.0, 0.0
@@ -220,21 +220,22 @@ def make_device_mf(nao=1000, nc=99, no=2, naux=None, ngrid=None, xctype="GGA", h
         t = torch.randn((q1 - q0, nao, nao), dtype=torch.float64, device=dev, generator=gaux)
         cderi[q0:q1] = (t + t.transpose(1, 2)) * s * dmat
         del t
-    ncomp = 4 if xctype == "GGA" else 1
+    ncomp = 4 if xctype in ("GGA", "MGGA") else 1
+    nf = 5 if xctype == "MGGA" else ncomp              # kernel components (+ tau)
     ng = g1 - g0
     scale = grid_scale(ngrid, nocc, nvir)
     ao = torch.randn((ncomp, ng, nao), dtype=torch.float64, device=dev, generator=g)
     ao.mul_(scale)
     w = torch.rand(ng, dtype=torch.float64, device=dev, generator=g) / ngrid
-    n = 2 * ncomp
+    n = 2 * nf
     f = torch.randn((n, n, ng), dtype=torch.float64, device=dev, generator=g) * 0.01
     f = 0.5 * (f + f.transpose(0, 1))
     for sa in range(2):
         for sb in range(2):
             v = -(0.1 + 0.9 * torch.rand(ng, dtype=torch.float64, device=dev, generator=g))
-            f[sa * ncomp, sb * ncomp] = v
-            f[sb * ncomp, sa * ncomp] = v
-    fxc = f.reshape(2, ncomp, 2, ncomp, ng).contiguous()
+            f[sa * nf, sb * nf] = v
+            f[sb * nf, sa * nf] = v
+    fxc = f.reshape(2, nf, 2, nf, ng).contiguous()
     fxc_sf = -(0.1 + 0.9 * torch.rand(ng, dtype=torch.float64, device=dev, generator=g)) * w
     small.cderi = cderi
     small.grids = Grid(ao=ao, weights=w)
