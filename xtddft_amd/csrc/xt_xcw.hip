@@ -8,20 +8,31 @@
 // K = occupied i.  A block covers 8 trial pairs and 64 grid points; each of its 8
 // waves owns one pair (one block per CU):
 //   * A = Zp[i][xg][a] (16 contiguous a per fragment row): loaded straight from
-//     global memory into registers through a 4-k-step ring (each wave's own pairs);
-//   * B = PhiO[g][i]: the block's 16 TNG x O tile, loaded ONCE per block into LDS
-//     and resident for the whole a loop;
+//     global memory into registers through a 4-slot ring, 3 k-steps ahead;
+//   * B = PhiO[g][i]: the block's 64 x O tile, loaded ONCE per block into LDS and
+//     resident for the whole a loop;
 //   * after each 32-wide a-tile's K loop the accumulators T[a][g] are contracted
 //     with dPhiV_c[g][a] (staged per a-tile in LDS, shared by the block's waves)
-//     into per-lane partial sums racc[j][c] -- the
-//     sum over a stays in-lane (rows a of a lane are q + 4 reg + 16 t) and only the
-//     final 4-row reduction crosses lanes, once per block.
-// One barrier per a-tile (26 k-steps x 8 MFMAs per wave at O = 101).
-// LDS images are [row][g] with g XOR-swizzled by h(row) = (row & 15) | (row & 1) << 4:
-// the global loads run along the row index (coalesced), so 16 lanes of a
-// ds_write_b64 group write 16 consecutive rows at one g -> 16 distinct bank pairs;
-// the fragment / weight reads (16 consecutive g, two rows of opposite parity per
-// 32-lane group) land in opposite bank halves.
+//     into per-lane partial sums racc[j][c] -- the sum over a stays in-lane (rows a
+//     of a lane are q + 4 reg + 16 t) and only the final 4-row reduction crosses
+//     lanes, once per block.
+//
+// Built for the FP64 issue model measured on gfx950 (tools/mfma_probe2.hip): every VALU
+// instruction in the MFMA stream costs its issue cycles to the matrix pipe (4 integer adds
+// per 8 MFMAs: -2.6 %; 4 v_mov_b64: -8 %), while LDS reads at immediate offsets are free
+// (-1 %).  So the hot loop carries no per-step VALU at all:
+//   * k index permutation: lane q of k-step pair p supplies i = 8 p + 2 q + (step & 1),
+//     so one ds_read_b128 per 16-column sub-tile feeds two k-steps;
+//   * LDS images are padded, not XOR-swizzled, so every address is a lane base plus a
+//     compile-time offset: PhiO [g][i] with pitch KI + 4 (= 4 mod 8 doubles: the four
+//     16-lane ds_read_b128 groups cover all 64 banks), weights [c][g][a] with pitch 34
+//     (32-lane ds_read_b64 groups conflict-free, 16-lane write runs contiguous);
+//   * global addresses are a wave-uniform base (SGPRs, scalar arithmetic) plus a fixed
+//     32-bit lane offset;
+//   * the first k-step of an a-tile multiplies into a zero accumulator (no 32-move reset);
+//   * ring slots and weight buffers are compile-time in every unrolled a-tile (a-tiles
+//     run in pairs when the ring phase alternates), so no register rotation.
+// One barrier per a-tile.
 #include <hip/hip_runtime.h>
 #include <mutex>
 #include <type_traits>
@@ -31,14 +42,23 @@ namespace xt {
 
 #define XT_INLINE __attribute__((always_inline))
 typedef double d4w __attribute__((ext_vector_type(4)));
+typedef double d2w __attribute__((ext_vector_type(2)));
 
 constexpr int WA = 32;           // virtuals per a-tile (2 MFMA row sub-tiles)
 constexpr int TMA = WA / 16;
-constexpr int WXB = 8;           // trial pairs per block (one per wave)
-constexpr int ZD = 4;            // Zp prefetch ring depth (k-steps; 2 measured +6.5 %, 6 +2.8 %, 8 spills)
+constexpr int WXB = 8;           // waves per block
+constexpr int ZD = 4;            // Zp ring slots (loads ZD - 1 k-steps ahead; 2 slots measured +6.5 %, 8 spills)
 constexpr int TNG = 4;           // 16-point column sub-tiles per block (64 grid points)
+constexpr int GB = 16 * TNG;     // grid points per block
+constexpr int WP = WA + 2;       // weight image pitch (doubles)
+constexpr int W_IMG = 3 * GB * WP;   // one weight buffer (doubles)
 
-__device__ __forceinline__ int swz(int row) { return (row & 15) | ((row & 1) << 4); }
+// PhiO image pitch (doubles): 4 mod 8 for conflict-free ds_read_b128 groups, compile-time so
+// the 16-column sub-tile offsets are immediates; the image holds KI = O rounded up to 8 <= 112
+// rows (O <= 112), and with two weight buffers fills the 160 KB exactly
+constexpr int PP = 116;
+constexpr int RHO_W_MAX_O = 112;
+__host__ __device__ constexpr int rho_w_ki(int O) { return (O + 7) & ~7; }   // occupied rows (k-step pairs whole)
 
 // transposing 4-row sum (lanes l, l^16, l^32, l^48): every lane ends with the total
 __device__ __forceinline__ double rows4(double v) {
@@ -53,10 +73,24 @@ __device__ __forceinline__ double rows4(double v) {
   return pair(pair(v, false), true);
 }
 
+// buffer descriptor over a wave-uniform base (readfirstlane'd so the compiler can prove it:
+// cdna_hip_programming.md T20); loads through it take a 32-bit lane offset and a scalar one,
+// so no 64-bit address arithmetic runs on the VALU
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const double* p) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+__device__ __forceinline__ double bld8(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+
 // PB trial pairs per block (8, 4, 2, 1; Davidson steps with few new vectors): the
-// H = 8 / PB waves of a pair split each a-tile's k-steps into H even ranges, contract
-// their partial T with the same staged weights (the contraction is linear in T) and
-// their partial sums are added through LDS once at the end -- every wave of the block
+// H = 8 / PB waves of a pair split each a-tile's k-step pairs into H even ranges,
+// contract their partial T with the same staged weights (the contraction is linear in T)
+// and add their partial sums through LDS once at the end -- every wave of the block
 // works when nx < 8, and the weight staging stays one image per a-tile.
 template <int PB>
 __global__ void __launch_bounds__(64 * WXB) __attribute__((amdgpu_waves_per_eu(2, 2)))
@@ -65,17 +99,13 @@ k_xc_rho_w(int O, int nx, int V, int n,
            const double* __restrict__ Z, long zi, long zx,
            const double* __restrict__ Wg, long wc, long wg,
            double* __restrict__ Rout, long rg) {
-  constexpr int GB = 16 * TNG;                 // grid points per block
-  constexpr int W_IMG = 3 * WA * GB;           // one weight buffer (doubles)
   constexpr int NT = 64 * WXB;                 // threads per block
-  // each a-tile's weights are staged in two halves (loaded before / stored after each half
-  // of the K loop), 6 staging registers instead of 12
-  constexpr int W_LD = W_IMG / NT / 2;         // weight elements staged per thread and half
-  static_assert(W_IMG % (2 * NT) == 0, "weight staging map");
+  constexpr int W_LD = 3 * GB * WA / NT;       // weight elements staged per thread and a-tile (12)
+  static_assert(3 * GB * WA == W_LD * NT && GB * WA / NT == 4, "weight staging map");
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int KI = (O + 7) & ~7;                 // occupied rows in the image (k-steps even)
-  double* sP = sm;                             // [KI][GB]
-  double* sW = sm + KI * GB;                   // [2][3][WA][GB]
+  const int KI = rho_w_ki(O);
+  double* sP = sm;                             // [GB][PP]
+  double* sW = sm + GB * PP;                   // [2][3][GB][WP]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -90,73 +120,73 @@ k_xc_rho_w(int O, int nx, int V, int n,
     const int xcd = lid & 7, idx = lid >> 3, qn = nblk >> 3, rem = nblk & 7;
     lid = xcd * qn + (xcd < rem ? xcd : rem) + idx;
   }
-  // (trial-pair sets of one g-tile side by side instead, sharing its gradient weights
-  // in L2: neutral, 168.1-168.3 vs 168.2-168.6 ms/step)
   constexpr int H = WXB / PB;                  // waves per pair
   const int gt = lid % ntg, xs = lid / ntg;
   const int g0 = gt * GB, x0 = xs * PB;
   const int pl = wave % PB, h = wave / PB;
   const int xg = x0 + pl;                      // this wave's trial pair
   const int nat = (V + WA - 1) / WA;
-  const int KS = KI / 4;
-  // this wave's k-steps of every a-tile: [s_lo, s_hi), even bounds (the ring phase stays even)
-  const int s_lo = H == 1 ? 0 : 2 * ((h * (KS / 2)) / H), s_hi = H == 1 ? KS : 2 * (((h + 1) * (KS / 2)) / H);
-  const bool wave_on = H == 1 ? xg < nx : (xg < nx && s_hi > s_lo);
+  const int KP = KI / 8;                       // k-step pairs per a-tile
+  // this wave's k-step pairs of every a-tile: [p_lo, p_hi)
+  const int p_lo = H == 1 ? 0 : (h * KP) / H, p_hi = H == 1 ? KP : ((h + 1) * KP) / H;
+  const int np = p_hi - p_lo;
+  const bool wave_on = xg < nx && np > 0;
 
-  // ---- PhiO tile -> LDS (once) ----------------------------------------------
+  // ---- PhiO tile -> LDS (once; rows past n read the zeroed grid slack) ----------
   for (int p = tid; p < KI * GB; p += NT) {
     const int g = p / KI, i = p % KI;
-    const double v = i < O ? PO[(long)(g0 + g) * ldp + i] : 0.0;   // rows past n: zeroed slack
-    sP[i * GB + (g ^ swz(i))] = v;
+    sP[g * PP + i] = i < O ? PO[(long)(g0 + g) * ldp + i] : 0.0;
   }
   // ---- weights of a-tile `at` (global -> registers -> LDS) -------------------
+  // thread element k (0..11): plane c = k / 4, grid row wr + 16 (k % 4), column wa.
+  // Columns past V read the next grid row (the arrays are row-padded and followed by
+  // XC_GRID_SLACK rows) and are stored as zero.
+  const int wa = tid & (WA - 1), wr = tid / WA;
+  const unsigned w_off = (unsigned)(((long)wr * wg + wa) * 8);
+  const __amdgpu_buffer_rsrc_t wrs[3] = {rsrc_of(Wg + (long)g0 * wg), rsrc_of(Wg + wc + (long)g0 * wg),
+                                         rsrc_of(Wg + 2 * wc + (long)g0 * wg)};
   double rw[W_LD];
-  auto load_w = [&](int at, int ph) XT_INLINE {
+  auto load_w = [&](int at) XT_INLINE {
 #pragma unroll
-    for (int e = 0; e < W_LD; ++e) {
-      const int p = tid + NT * (e + ph * W_LD), c = p / (WA * GB), g = (p / WA) % GB, a = p % WA;
-      rw[e] = Wg[c * wc + (long)(g0 + g) * wg + min(at * WA + a, V - 1)];
+    for (int k = 0; k < W_LD; ++k) rw[k] = bld8(wrs[k / 4], w_off, (int)((16 * (k % 4) * wg + (long)at * WA) * 8));
+  };
+  double* const w_st = sW + wr * WP + wa;
+  auto store_w = [&](auto BUF, int at) XT_INLINE {
+    constexpr int B = decltype(BUF)::value;
+    if ((at + 1) * WA <= V) {
+#pragma unroll
+      for (int k = 0; k < W_LD; ++k) w_st[B * W_IMG + ((k / 4) * GB + 16 * (k % 4)) * WP] = rw[k];
+    } else {
+      const bool live = at * WA + wa < V;
+#pragma unroll
+      for (int k = 0; k < W_LD; ++k) w_st[B * W_IMG + ((k / 4) * GB + 16 * (k % 4)) * WP] = live ? rw[k] : 0.0;
     }
   };
-  auto store_w = [&](int buf, int at, int ph) XT_INLINE {
-#pragma unroll
-    for (int e = 0; e < W_LD; ++e) {
-      const int p = tid + NT * (e + ph * W_LD), c = p / (WA * GB), g = (p / WA) % GB, a = p % WA;
-      sW[buf * W_IMG + (c * WA + a) * GB + (g ^ swz(a))] = at * WA + a < V ? rw[e] : 0.0;
-    }
-  };
-  load_w(0, 0);
-  store_w(0, 0, 0);
-  load_w(0, 1);
-  store_w(0, 0, 1);
+  load_w(0);
+  store_w(std::integral_constant<int, 0>{}, 0);
 
-  // ---- Zp ring: k-step u of the whole a loop (a-tile u / KS, k-step u % KS) ----
-  // lane (q, r16) loads rows i = 4 s + q (past O: zeroed slack rows of Zp) of
-  // columns at WA + 16 t + r16 (past V: the next pair's values, weighted by zero)
-  const double* zb = Z + (long)(wave_on ? xg : 0) * zx + r16 + (long)q * zi;
+  // ---- Zp ring: lane (q, r16) of k-step s supplies row i = 8 (s / 2) + 2 q + (s & 1)
+  // (past O: zeroed slack rows of Zp) of columns at WA + 16 t + r16 (past V: the next
+  // pair's values, weighted by zero).  The walker (zs, za) is the next k-step to load:
+  // past the wave's last k-step of an a-tile it moves to its first k-step of the next
+  // tile (the last tile repeats itself: those loads are never consumed).
+  const __amdgpu_buffer_rsrc_t zrs = rsrc_of(Z + (long)(wave_on ? xg : 0) * zx);
+  const unsigned z_off = (unsigned)(((long)2 * q * zi + r16) * 8);
   double zq[ZD][TMA];
-  const long zstep = 4 * zi;
-  const double* zn = H == 1 ? zb : zb + s_lo * zstep;   // next k-step to load: a-tile za, k-step zs
-  int zs = s_lo, za = 0;
-  // advance to the next k-step; past the wave's last k-step of an a-tile the pointer jumps
-  // to its first k-step of the next tile (the last tile repeats itself: those loads are
-  // never consumed).  An if/else, which splits the unrolled K loop into one basic block
-  // per k-step (a select-based form with one block per 4 k-steps measured 4 % slower).
+  const int s_lo = 2 * p_lo, s_hi = 2 * p_hi;
+  const int z_lo = 8 * p_lo * (int)zi * 8;     // byte offset of row 8 p_lo (scalar)
+  int zs = s_lo, za = 0, zso = z_lo;           // zso: byte offset of k-step zs's rows in a-tile za
   auto load_z = [&](int slot) XT_INLINE {
 #pragma unroll
-    for (int t = 0; t < TMA; ++t) zq[slot][t] = zn[16 * t];
-    if constexpr (H == 1) {
-      if (++zs == KS) { zs = 0; za = za + 1 < nat ? za + 1 : za; zn = zb + za * WA; }
-      else zn += zstep;
+    for (int t = 0; t < TMA; ++t) zq[slot][t] = bld8(zrs, z_off + 128 * t, zso);
+    if (++zs == s_hi) {
+      zs = s_lo;
+      za = za + 1 < nat ? za + 1 : za;
+      zso = za * WA * 8 + z_lo;
     } else {
-      if (++zs == s_hi) { zs = s_lo; za = za + 1 < nat ? za + 1 : za; zn = zb + za * WA + s_lo * zstep; }
-      else zn += zstep;
+      zso += (zs & 1 ? 1 : 7) * (int)zi * 8;   // rows 8 p + {0, 1} of a pair, then the next pair
     }
   };
-  if (H == 1 || wave_on) {   // (a wave with no k-steps must not walk the ring)
-#pragma unroll
-    for (int d = 0; d < ZD; ++d) load_z(d);
-  }
 
   d4w acc[TMA][TNG];
   double racc[TNG][3];
@@ -165,102 +195,102 @@ k_xc_rho_w(int O, int nx, int V, int n,
 #pragma unroll
     for (int c = 0; c < 3; ++c) racc[j][c] = 0.0;
 
-  const int p_lane = q * GB;                   // B image: row 4 s + q, column (16 j + r16) ^ swz
-  // B fragments one k-step ahead: step s reads bq[s & 1] and loads step s + 1's into
-  // bq[(s + 1) & 1] before its MFMAs, so their LDS latency hides under this step's
-  // matrix work (a read past the last k-step lands in the weight image: unused)
-  double bq[2][TNG];
-  auto bload = [&](int s, double* dst) XT_INLINE {
-    const int sw = swz(4 * s + q);
+  // B fragments of k-step pair p: columns 16 j + r16, rows 8 p + 2 q + {0, 1}
+  d2w bq[2][TNG];
+  const double* const b_lane = sP + r16 * PP + 2 * q;
+  auto bread = [&](int p, d2w* dst) XT_INLINE {
+    const d2w* src = (const d2w*)(b_lane + 8 * p);
 #pragma unroll
-    for (int j = 0; j < TNG; ++j) dst[j] = sP[p_lane + 4 * s * GB + ((16 * j + r16) ^ sw)];
+    for (int j = 0; j < TNG; ++j) dst[j] = src[(16 * j * PP) / 2];
   };
-  // one k-step from ring slot `slot` and B buffer `bb` (compile-time after unrolling)
-  auto step = [&](int s, int slot, int bb) XT_INLINE {
-    bload(s + 1, bq[bb ^ 1]);
-    double af[TMA];
-#pragma unroll
-    for (int t = 0; t < TMA; ++t) af[t] = zq[slot][t];
-    load_z(slot);
+  // one k-step from ring slot SL and B buffer BB, half SUB of the pair; ZERO: the first
+  // k-step of the a-tile, into a zero accumulator
+  auto step = [&](auto SL, auto BB, auto SUB, auto ZERO) XT_INLINE {
+    constexpr int sl = decltype(SL)::value, bb = decltype(BB)::value, sub = decltype(SUB)::value;
+    load_z((sl + ZD - 1) % ZD);   // into the slot the previous k-step consumed
 #pragma unroll
     for (int t = 0; t < TMA; ++t)
 #pragma unroll
       for (int j = 0; j < TNG; ++j)
-        acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t], bq[bb][j], acc[t][j], 0, 0, 0);
+        acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+            zq[sl][t], bq[bb][j][sub], decltype(ZERO)::value ? (d4w){0.0, 0.0, 0.0, 0.0} : acc[t][j], 0, 0, 0);
   };
-  // the K loop of one a-tile whose first k-step sits in ring slot PH (KS is even, so
-  // PH is even); the slots stay compile-time constants inside each unrolled group
-  auto kloop = [&](auto PH, int s0, int s1) XT_INLINE {
-    constexpr int P = decltype(PH)::value;
-    bload(s0, bq[0]);
-    int s = s0;
-    for (; s + ZD <= s1; s += ZD) {
-#pragma unroll
-      for (int d = 0; d < ZD; ++d) step(s + d, (P + d) % ZD, d & 1);
-    }
-#pragma unroll
-    for (int d = 0; d < ZD; ++d)
-      if (s + d < s1) step(s + d, (P + d) % ZD, d & 1);
+  // one k-step pair in ring slots SL, SL + 1 from B buffer BB; prefetches pair pn's B
+  auto kpair = [&](auto SL, auto BB, auto ZERO, int pn) XT_INLINE {
+    constexpr int sl = decltype(SL)::value, bb = decltype(BB)::value;
+    bread(pn, bq[bb ^ 1]);
+    step(std::integral_constant<int, sl>{}, BB, std::integral_constant<int, 0>{}, ZERO);
+    step(std::integral_constant<int, (sl + 1) % ZD>{}, BB, std::integral_constant<int, 1>{},
+         std::integral_constant<bool, false>{});
   };
-  // k-steps [s0, s1) of a-tile at (s0 even: the ring phase stays even)
-  auto krange = [&](int at, int s0, int s1) XT_INLINE {
-    static_assert(ZD == 4, "ring phases");
-    const int ph = H == 1 ? (int)(((long)at * KS + s0) % ZD) : (int)(((long)at * (s_hi - s_lo) + s0 - s_lo) % ZD);
-    if (ph == 0) kloop(std::integral_constant<int, 0>{}, s0, s1);
-    else         kloop(std::integral_constant<int, 2>{}, s0, s1);
-  };
-  __syncthreads();
-  const int s_mid = s_lo + (((s_hi - s_lo) / 2) & ~1);
-  for (int at = 0; at < nat; ++at) {
-    const int buf = at & 1;
-    if (at + 1 < nat) load_w(at + 1, 0);
-#pragma unroll
-    for (int t = 0; t < TMA; ++t)
-#pragma unroll
-      for (int j = 0; j < TNG; ++j) acc[t][j] = (d4w){0.0, 0.0, 0.0, 0.0};
-    if (at + 1 < nat) {
-      store_w(buf ^ 1, at + 1, 0);
-      load_w(at + 1, 1);
-    }
+  using F = std::integral_constant<bool, false>;
+  using T1 = std::integral_constant<bool, true>;
+
+  // one a-tile: ring phase P (slot of its first k-step) and weight buffer BUF compile-time
+  auto tile = [&](auto PH, auto BUF, int at) XT_INLINE {
+    constexpr int P = decltype(PH)::value, B = decltype(BUF)::value;
+    if (at + 1 < nat) load_w(at + 1);
     if (wave_on) {
-      krange(at, s_lo, s_hi);
+      kpair(std::integral_constant<int, P>{}, std::integral_constant<int, 0>{}, T1{}, p_lo + 1);
+      int k = 1;
+      for (; k + 2 <= np; k += 2) {
+        kpair(std::integral_constant<int, (P + 2) % ZD>{}, std::integral_constant<int, 1>{}, F{}, p_lo + k + 1);
+        kpair(std::integral_constant<int, P>{}, std::integral_constant<int, 0>{}, F{}, p_lo + k + 2);
+      }
+      if (k < np) kpair(std::integral_constant<int, (P + 2) % ZD>{}, std::integral_constant<int, 1>{}, F{}, p_lo + k + 1);
+      bread(p_lo, bq[0]);        // the next a-tile's first pair (the PhiO image never changes)
       // contraction with the a-tile's weights: acc[t][j][r] = T[a = 16 t + q + 4 r][g = 16 j + r16].
       // Half a row (t, r) of weights at a time, the next half's reads issued before this
-      // half's FMAs (two 6-value buffers; unfenced, the compiler hoists all 96 reads and
-      // spills; fenced without the lookahead, every row waits out the LDS latency)
-      const double* w = sW + buf * W_IMG;
-      constexpr int JH = TNG / 2;                // half a row: JH column sub-tiles x 3 weights
+      // half's FMAs (two 6-value buffers; unfenced, the compiler hoists all 96 reads)
+      const double* w = sW + B * W_IMG + r16 * WP + q;
+      constexpr int JH = TNG / 2;
       double wb[2][JH * 3];
-      auto wread = [&](int h, double* dst) XT_INLINE {
-        const int rw = h / 2, j0 = (h % 2) * JH;
-        const int t = rw / 4, r = rw % 4;
-        const int a = 16 * t + q + 4 * r;
-        const int sa = swz(a);
+      auto wread = [&](int hh, double* dst) XT_INLINE {
+        const int rw_ = hh / 2, j0 = (hh % 2) * JH;
+        const int t = rw_ / 4, r = rw_ % 4;
 #pragma unroll
-        for (int jj = 0; jj < JH; ++jj) {
-          const int col = (16 * (j0 + jj) + r16) ^ sa;
+        for (int jj = 0; jj < JH; ++jj)
 #pragma unroll
-          for (int c = 0; c < 3; ++c) dst[3 * jj + c] = w[(c * WA + a) * GB + col];
-        }
+          for (int c = 0; c < 3; ++c) dst[3 * jj + c] = w[(c * GB + 16 * (j0 + jj)) * WP + 16 * t + 4 * r];
       };
       wread(0, wb[0]);
 #pragma unroll
-      for (int h = 0; h < 8 * TMA; ++h) {
-        if (h + 1 < 8 * TMA) wread(h + 1, wb[(h + 1) & 1]);
-        const int rw = h / 2, j0 = (h % 2) * JH;
-        const int t = rw / 4, r = rw % 4;
+      for (int hh = 0; hh < 8 * TMA; ++hh) {
+        if (hh + 1 < 8 * TMA) wread(hh + 1, wb[(hh + 1) & 1]);
+        const int rw_ = hh / 2, j0 = (hh % 2) * JH;
+        const int t = rw_ / 4, r = rw_ % 4;
 #pragma unroll
         for (int jj = 0; jj < JH; ++jj)
 #pragma unroll
           for (int c = 0; c < 3; ++c)
-            racc[j0 + jj][c] += acc[t][j0 + jj][r] * wb[h & 1][3 * jj + c];
+            racc[j0 + jj][c] += acc[t][j0 + jj][r] * wb[hh & 1][3 * jj + c];
         __builtin_amdgcn_sched_barrier(0);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (at + 1 < nat) store_w(buf ^ 1, at + 1, 1);
+    if (at + 1 < nat) store_w(std::integral_constant<int, B ^ 1>{}, at + 1);
     __syncthreads();
+  };
+
+  __syncthreads();
+  if (wave_on) {
+#pragma unroll
+    for (int d = 0; d < ZD - 1; ++d) load_z(d);
+    bread(p_lo, bq[0]);
   }
+  // a-tiles in pairs: with an odd pair count per a-tile the ring phase alternates 0, 2
+  auto run = [&](auto ALT) XT_INLINE {
+    constexpr int P1 = decltype(ALT)::value ? 2 : 0;
+    int at = 0;
+    for (; at + 2 <= nat; at += 2) {
+      tile(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, at);
+      tile(std::integral_constant<int, P1>{}, std::integral_constant<int, 1>{}, at + 1);
+    }
+    if (at < nat) tile(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, at);
+  };
+  if (np & 1) run(T1{});
+  else run(F{});
+
   if constexpr (H > 1) {
     // the H waves of a pair hold partial sums over disjoint k-ranges: add them through
     // LDS (the weight buffers are free after the last barrier)
@@ -298,8 +328,7 @@ k_xc_rho_w(int O, int nx, int V, int n,
 // two trial pairs per wave on 32-point blocks (163.3 vs 168.5 on one box, 170.0 vs 168.9
 // on another: not reproducible); two pairs per wave on 64-point blocks (spills, 345).
 static size_t rho_w_lds(int O) {
-  constexpr int GB = 16 * TNG;
-  return sizeof(double) * ((size_t)((O + 7) & ~7) * GB + 2 * 3 * WA * GB);
+  return O > RHO_W_MAX_O ? (size_t)1 << 40 : sizeof(double) * ((size_t)GB * PP + 2 * W_IMG);
 }
 
 size_t xc_rho_w_lds_bytes(int O) { return rho_w_lds(O); }
@@ -317,14 +346,15 @@ static void lds_attribute(K kern, int slot) {
   if (dev < 64) done[slot] |= 1ull << dev;
 }
 
-// pairs per block: relative block time ~ PB / 8 (the k-steps each wave runs) + 0.13 (the
-// per-a-tile contraction, staging and barrier, ~21 of 168 ms at PB 8), times the blocks
-// per grid tile; the cheapest wins
+// pairs per block: relative block time ~ PB / 8 (the k-steps each wave runs) + 0.27 (the
+// per-a-tile contraction, staging and barrier; fitted to the nvec sweep of the VALU-free
+// kernel: a 4-pair block costs 0.60, a 2-pair block 0.415 of an 8-pair block), times the
+// blocks per grid tile; the cheapest wins
 static int rho_w_pb(int nx) {
   int best = 8;
   double best_cost = 1e30;
   for (int pb = 8; pb >= 1; pb /= 2) {
-    const double cost = (double)((nx + pb - 1) / pb) * (pb / 8.0 + 0.13);
+    const double cost = (double)((nx + pb - 1) / pb) * (pb / 8.0 + 0.27);
     if (cost < best_cost - 1e-9) { best_cost = cost; best = pb; }
   }
   return best;
@@ -335,7 +365,6 @@ int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const doub
   if (O <= 0 || nx <= 0 || V <= 0 || n <= 0) return 0;
   const size_t lds = rho_w_lds(O);
   if (lds > 160 * 1024) return XT_ERR_ARG;
-  constexpr int GB = 16 * TNG;
   const int ntg = (n + GB - 1) / GB;
   const int pb = rho_w_pb(nx);
   const int blocks = ntg * ((nx + pb - 1) / pb);
