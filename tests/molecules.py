@@ -34,9 +34,11 @@ def hf_scf(kind: str):
     """Converged SCF object: 'ROKS' / 'UKS' with the notebook's irrep_nelec,
     'ROKS_AUFBAU' = example/spin up.ipynb (H 0 0 0; F 0 0 1.0, no constraint);
     'ROKS_TPSS' / 'UKS_TPSS': the same molecule with the TPSS meta-GGA (unpinned
-    energy; the source of the MGGA response checks)."""
-    if kind.endswith("_TPSS"):
-        mf = (ROKS if kind.startswith("ROKS") else UKS)(hf_mol(), "tpss")
+    energy; the source of the MGGA response checks); 'ROKS_CAMB3LYP' / 'UKS_CAMB3LYP'
+    with the range-separated CAM-B3LYP (unpinned; the long-range exchange checks)."""
+    if kind.endswith("_TPSS") or kind.endswith("_CAMB3LYP"):
+        xc = "tpss" if kind.endswith("_TPSS") else "cam-b3lyp"
+        mf = (ROKS if kind.startswith("ROKS") else UKS)(hf_mol(), xc)
         mf.irrep_nelec = dict(HF_IRREP_NELEC)
         mf.conv_tol = 1e-11
         mf.kernel()

@@ -455,3 +455,82 @@ def test_tpss_roks_scf_converges():
     mf = hf_scf("ROKS_TPSS")
     assert mf.converged and mf.xctype == "MGGA"
     assert abs(mf.e_tot - reference_outputs()["roks_bhandhlyp_e_tot"]) < 0.1
+
+
+def test_erf_attenuation_limits_and_series():
+    """att(a) of the short-range (erf-screened) exchange hole (qc/xc.py, libxc
+    attenuation_erf): att -> 1 as omega -> 0 (full B88), -> 1/(36 a^2) as omega -> inf,
+    and the large-a series agrees with the closed form where both are accurate, with
+    continuous first and second derivatives at the switch."""
+    import math
+    import torch
+    from xtddft_amd.qc import xc
+
+    def closed(a):
+        return 1 - 8 / 3 * a * (math.sqrt(math.pi) * math.erf(1 / (2 * a))
+                                + (2 * a - 4 * a ** 3) * math.exp(-1 / (4 * a * a)) - 3 * a + 4 * a ** 3)
+    a = torch.tensor([1e-4, 1e-2, 0.1, 0.3, 0.59, 0.61, 0.8, 1.2], dtype=torch.float64)
+    att = xc._att_erf(a, torch).numpy()
+    ref = np.array([closed(v) for v in a.tolist()])
+    assert abs(att[0] - (1.0 - 8.0 / 3.0 * math.sqrt(math.pi) * 1e-4)) < 1e-7   # att = 1 - 8/3 sqrt(pi) a + O(a^2)
+    assert np.abs(att - ref).max() < 1e-13
+    big = torch.tensor([50.0, 500.0], dtype=torch.float64)
+    tail = xc._att_erf(big, torch).numpy()
+    bn = big.numpy()
+    assert np.allclose(tail, 1 / (36 * bn ** 2) - 1 / (960 * bn ** 4) + 1 / (26880 * bn ** 6), rtol=1e-12, atol=0)
+    x = torch.tensor([xc._ATT_SWITCH - 1e-9, xc._ATT_SWITCH + 1e-9], dtype=torch.float64, requires_grad=True)
+    y = xc._att_erf(x, torch)
+    g = torch.autograd.grad(y.sum(), x, create_graph=True)[0]
+    h = torch.autograd.grad(g.sum(), x)[0]
+    dx = float(x[0] - x[1])
+    assert abs(float(y[0] - y[1]) - float(g[0]) * dx) < 1e-14
+    assert abs(float(g[0] - g[1]) - float(h[0]) * dx) < 1e-12
+    assert abs(float(h[0] - h[1])) < 1e-6
+
+
+def test_camb3lyp_coefficients_and_b88_limit():
+    """CAM-B3LYP's (omega, alpha, hyb) as PySCF returns them, and the ITYH short-range
+    B88 reaching the full B88 as omega -> 0 (per spin, GGA points)."""
+    import torch
+    from xtddft_amd.qc import xc
+    assert xc.rsh_and_hybrid_coeff("CAM-B3LYP") == (0.33, 0.65, 0.19)
+    assert xc.rsh_and_hybrid_coeff("B3LYP") == (0.0, 0.2, 0.2)
+    rng = np.random.default_rng(3)
+    t = lambda v: torch.tensor(v, dtype=torch.float64)
+    ra, rb = t(rng.uniform(0.05, 3, 40)), t(rng.uniform(0.05, 3, 40))
+    saa, sbb = t(rng.uniform(0, 2, 40)), t(rng.uniform(0, 2, 40))
+    z = torch.zeros_like(ra)
+    full = xc._b88(ra, rb, saa, z, sbb, torch)
+    sr0 = xc._ityh_b88(ra, rb, saa, z, sbb, torch, 1e-7)
+    sr_big = xc._ityh_b88(ra, rb, saa, z, sbb, torch, 1e4)
+    assert torch.allclose(sr0, full, rtol=1e-6)
+    assert float(sr_big.abs().max()) < 1e-6 * float(full.abs().max())
+
+
+@pytest.mark.parametrize("kind", ["ROKS", "UKS"])
+def test_camb3lyp_scf_energy_is_stationary(kind):
+    """Range-separated SCF (CAM-B3LYP, K = hyb K + (alpha - hyb) K_LR): the energy is the
+    functional whose derivative is the Fock matrix -- central differences of
+    E[D0 + e Delta] along a symmetric perturbation equal sum_s tr(F_s Delta_s), which pins
+    the long-range exchange's energy factor and potential together; the SCF converges.
+    Parity unpinned (no reference printout with a range-separated functional)."""
+    from molecules import hf_scf
+    mf = hf_scf(f"{kind}_CAMB3LYP")
+    assert mf.converged and mf.omega == 0.33 and mf.eri_lr is not None
+    d0 = np.asarray(mf._dm)
+    rng = np.random.default_rng(5)
+    dl = rng.normal(size=d0.shape) * 1e-2
+    dl = dl + dl.transpose(0, 2, 1)
+
+    def etot(d):
+        parts = mf.get_veff(dm=d)
+        return mf.energy_elec(d, parts)[0]
+    veff = mf.get_veff(dm=d0)[0]
+    grad = sum(np.sum((mf.h1e + veff[s]) * dl[s]) for s in range(2))
+    eps = 1e-4
+    fd = (etot(d0 + eps * dl) - etot(d0 - eps * dl)) / (2 * eps)
+    assert abs(fd - grad) < 1e-7 * max(1.0, abs(grad))
+    # the long-range part is really there: K_LR differs from K and from zero
+    klr = mf.get_k_lr(d0)
+    k = mf.get_jk(dm=d0)[1]
+    assert 0.05 < np.abs(klr).max() < np.abs(k).max()

@@ -987,7 +987,12 @@ static int xc_response(xt_ctx* c, int nz) {
     for (int q = 0; q < ngr; ++q) {
       const int nzg = gr[q].nch * nz;
       Ug[q] = c->ubuf.p + (long)gr[q].ch0 * nz * O * n;  ldU[q] = (long)nzg * O;
-      Rg[q] = gga ? c->wbuf.p + (long)gr[q].ch0 * nz * 3 * n : nullptr;  ldR[q] = (long)nzg * 3;
+      // each group's wv block is followed by XC_GRID_SLACK zero rows (the M-backward
+      // kernel's last K-tile reads them instead of masking rows past n)
+      Rg[q] = gga ? c->wbuf.p + (long)gr[q].ch0 * nz * 3 * (n + XC_GRID_SLACK) : nullptr;  ldR[q] = (long)nzg * 3;
+      if (gga && hipMemsetAsync(Rg[q] + (long)n * ldR[q], 0, sizeof(double) * XC_GRID_SLACK * ldR[q], c->st) !=
+                     hipSuccess)
+        return fail(XT_ERR_HIP, "wv slack memset failed");
       const double* PV = c->Phi.p + gr[q].vb * basP + (long)g0 * nmo + c->v0;
       const double* PO = c->Phi.p + gr[q].ob * basP + (long)g0 * nmo;
       GemmDesc f1;   // U[g][(x,i)] = sum_a PhiV0[g][a] Ze[(x,i)][a]

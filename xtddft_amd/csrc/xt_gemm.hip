@@ -104,7 +104,7 @@ __device__ __forceinline__ void swap16_d(double& A, double& B) {
 // on one SIMD.  ROWSIMD (WGM = 4) takes wm = w % 4 instead: a ragged column edge then
 // spreads over all four SIMDs (a ragged row edge concentrates).
 template <int BM, int BN, int WGM, int WGN, int BK, int MINW, bool A_KC, bool B_KC, int TAG, int MODE = 0,
-          int MAP = 0, bool ROWSIMD = false>
+          int MAP = 0, bool ROWSIMD = false, bool KMASK = true>
 __global__ void __launch_bounds__(64 * WGM * WGN, MINW)
 dgemm_kernel(GemmParams p) {
   static_assert(MODE == 0 || ((BM == 128 || (MODE == 2 && BM == 64)) && WGM * WGN == 8 && !A_KC && B_KC),
@@ -259,17 +259,25 @@ dgemm_kernel(GemmParams p) {
   // Stage K-tile (r, kt) into registers.  Branch-free: k past K (last tile of
   // each r) reads k = 0 of the same row instead; the B copy of those k is
   // zeroed in store_tile, so they add nothing.  Returns the valid k count.
-  auto load_tile = [&](int r, int kt) XT_INLINE -> int {
+  // EDGE: the tile may reach past K (masked staging); !EDGE: a whole K-tile, staged with
+  // no per-element selects (the VALU issue cycles they cost come out of the FP64 matrix
+  // pipe, tools/mfma_probe2.hip)
+  auto load_tile = [&](auto EDGE, int r, int kt) XT_INLINE -> int {
+    constexpr bool edge = decltype(EDGE)::value;
     const int k0 = kt * BK;
     const int kv = p.K - k0;
     const char* At = (const char*)(Ab + (long)r * p.sAr + (A_KC ? (long)k0 : (long)k0 * p.sAk));
     const char* Bt = (const char*)(Bb + (long)r * p.sBr + (B_KC ? (long)k0 : (long)k0 * p.sBk));
+    // buffer loads off the tile's (block-uniform) origin: 32-bit lane offsets, no 64-bit
+    // address arithmetic on the VALU
+    const __amdgpu_buffer_rsrc_t ars = rsrc_of((const double*)At), brs = rsrc_of((const double*)Bt);
 #pragma unroll
     for (int e = 0; e < A_ELEMS; ++e) {
-      unsigned o;
-      if (A_KC) o = (a_fix < kv) ? aoff[e] : aoff[e] - (unsigned)(a_fix * 8);
+      unsigned o = aoff[e];
+      if (!edge) {}
+      else if (A_KC) o = (a_fix < kv) ? aoff[e] : aoff[e] - (unsigned)(a_fix * 8);
       else      o = (a_var + e * A_STEP < kv) ? aoff[e] : aoff[e] - (unsigned)((a_var + e * A_STEP) * p.sAk * 8);
-      ra[e] = *(const double*)(At + o);
+      ra[e] = bld8(ars, o, 0);
     }
     if constexpr (MODE == 2) {
       // generated operand: raw inputs of k row g (clamped to the tile's first row past K)
@@ -285,15 +293,17 @@ dgemm_kernel(GemmParams p) {
     } else {
 #pragma unroll
       for (int e = 0; e < B_ELEMS; ++e) {
-        unsigned o;
-        if (B_KC) o = (b_fix < kv) ? boff[e] : boff[e] - (unsigned)(b_fix * 8);
+        unsigned o = boff[e];
+        if (!edge) {}
+        else if (B_KC) o = (b_fix < kv) ? boff[e] : boff[e] - (unsigned)(b_fix * 8);
         else      o = (b_var + e * B_STEP < kv) ? boff[e] : boff[e] - (unsigned)((b_var + e * B_STEP) * p.sBk * 8);
-        rb[e] = *(const double*)(Bt + o);
+        rb[e] = bld8(brs, o, 0);
       }
     }
     return kv;
   };
-  auto store_tile = [&](int buf, int kv) XT_INLINE {
+  auto store_tile = [&](auto EDGE, int buf, int kv) XT_INLINE {
+    constexpr bool edge = decltype(EDGE)::value;
 #pragma unroll
     for (int e = 0; e < A_ELEMS; ++e) {
       int mm, kk;
@@ -314,7 +324,7 @@ dgemm_kernel(GemmParams p) {
       for (int e = 0; e < B_ELEMS; ++e) {
         int nn, kk;
         if (B_KC) { nn = b_var + e * B_STEP; kk = b_fix; } else { kk = b_var + e * B_STEP; nn = b_fix; }
-        smem[buf * STAGE + BM * LDP + nn * LDP + kk] = (kk < kv) ? rb[e] : 0.0;
+        smem[buf * STAGE + BM * LDP + nn * LDP + kk] = (!edge || kk < kv) ? rb[e] : 0.0;
       }
     }
   };
@@ -385,27 +395,66 @@ dgemm_kernel(GemmParams p) {
   // skips the k-steps past K.  Waves whose sub-tiles reach past M / N run the
   // MN_EDGE variant of the same loop (wave-uniform choice; both variants pass
   // the same barriers).
+  // KMASK: ragged K inside every reduce index (R > 1, BK does not divide K): every K-tile
+  // takes the masked staging.  Otherwise at most one K-tile is ragged (the last one, R == 1)
+  // and it runs FIRST, staged by the prologue: the pipelined loop then stages whole tiles
+  // only, with no per-element selects (the VALU issue cycles they cost come out of the
+  // FP64 matrix pipe, tools/mfma_probe2.hip) and no second loop body competing for the
+  // 128-register budget.  The order of the k sum changes, not its terms.
   auto run = [&](auto MN_EDGE) XT_INLINE {
-    int r = (int)(u0 / nkt), kt = (int)(u0 % nkt);
-    int kv = load_tile(r, kt);
-    store_tile(0, kv);
-    __syncthreads();
-    int buf = 0;
-    for (long u = u0; u + 1 < u1; ++u) {
-      int ktn = kt + 1, rn = r;
-      if (ktn == nkt) { ktn = 0; rn = r + 1; }
-      kv = load_tile(rn, ktn);
-      compute(buf, MN_EDGE, std::false_type{}, BK);
-      // keep the LDS stores (and their vmcnt waits) behind every MFMA of this
-      // tile: hoisted into the MFMA stream they stall it on global latency
-      // (measured: stores pinned mid-tile are 3-5 % slower)
-      __builtin_amdgcn_sched_barrier(0);
-      store_tile(buf ^ 1, kv);
+    if constexpr (KMASK) {
+      int r = (int)(u0 / nkt), kt = (int)(u0 % nkt);
+      int kv = load_tile(std::true_type{}, r, kt);
+      store_tile(std::true_type{}, 0, kv);
       __syncthreads();
-      r = rn; kt = ktn;
-      buf ^= 1;
+      int buf = 0;
+      for (long u = u0; u + 1 < u1; ++u) {
+        int ktn = kt + 1, rn = r;
+        if (ktn == nkt) { ktn = 0; rn = r + 1; }
+        kv = load_tile(std::true_type{}, rn, ktn);
+        compute(buf, MN_EDGE, std::false_type{}, BK);
+        // keep the LDS stores (and their vmcnt waits) behind every MFMA of this
+        // tile: hoisted into the MFMA stream they stall it on global latency
+        // (measured: stores pinned mid-tile are 3-5 % slower)
+        __builtin_amdgcn_sched_barrier(0);
+        store_tile(std::true_type{}, buf ^ 1, kv);
+        __syncthreads();
+        r = rn; kt = ktn;
+        buf ^= 1;
+      }
+      compute(buf, MN_EDGE, std::true_type{}, p.K - kt * BK);
+    } else {
+      const bool ragged = (p.K % BK != 0) && u1 == units;   // this split holds the ragged tile
+      const long first = ragged ? units - 1 : u0;
+      long u = ragged ? u0 : u0 + 1;                         // the rest: [u, rest_end)
+      const long rest_end = ragged ? units - 1 : u1;
+      const int kv0 = load_tile(std::true_type{}, (int)(first / nkt), (int)(first % nkt));
+      store_tile(std::true_type{}, 0, kv0);
+      __syncthreads();
+      if (u >= rest_end) {
+        compute(0, MN_EDGE, std::true_type{}, kv0);
+        return;
+      }
+      int r = (int)(u / nkt), kt = (int)(u % nkt);
+      int buf = 0;
+      // the first tile (ragged or whole) under the next one's staging
+      load_tile(std::false_type{}, r, kt);
+      compute(0, MN_EDGE, std::true_type{}, kv0);
+      __builtin_amdgcn_sched_barrier(0);
+      store_tile(std::false_type{}, 1, BK);
+      __syncthreads();
+      buf = 1;
+      for (++u; u < rest_end; ++u) {
+        if (++kt == nkt) { kt = 0; ++r; }
+        load_tile(std::false_type{}, r, kt);
+        compute(buf, MN_EDGE, std::false_type{}, BK);
+        __builtin_amdgcn_sched_barrier(0);
+        store_tile(std::false_type{}, buf ^ 1, BK);
+        __syncthreads();
+        buf ^= 1;
+      }
+      compute(buf, MN_EDGE, std::false_type{}, BK);
     }
-    compute(buf, MN_EDGE, std::true_type{}, p.K - kt * BK);
   };
   if constexpr (MODE == 1) {
     // rho forward: one a-block (16 a of the block's xg) per r; after its last
@@ -483,23 +532,23 @@ dgemm_kernel(GemmParams p) {
       }
     };
     auto run1 = [&](auto MN_EDGE) XT_INLINE {
-      int kv = load_tile(0, 0);
-      store_tile(0, kv);
+      int kv = load_tile(std::true_type{}, 0, 0);
+      store_tile(std::true_type{}, 0, kv);
       __syncthreads();
       int buf = 0;
       for (int r = 0; r < p.R; ++r) {
         for (int kt = 0; kt + 1 < nkt; ++kt) {
-          kv = load_tile(r, kt + 1);
+          kv = load_tile(std::true_type{}, r, kt + 1);
           compute(buf, MN_EDGE, std::false_type{}, BK);
           __builtin_amdgcn_sched_barrier(0);
-          store_tile(buf ^ 1, kv);
+          store_tile(std::true_type{}, buf ^ 1, kv);
           __syncthreads();
           buf ^= 1;
         }
-        kv = load_tile(r + 1 < p.R ? r + 1 : r, 0);   // first tile of the next a-block
+        kv = load_tile(std::true_type{}, r + 1 < p.R ? r + 1 : r, 0);   // first tile of the next a-block
         compute(buf, MN_EDGE, std::true_type{}, p.K - (nkt - 1) * BK);
         __builtin_amdgcn_sched_barrier(0);
-        store_tile(buf ^ 1, kv);
+        store_tile(std::true_type{}, buf ^ 1, kv);
         __syncthreads();
         buf ^= 1;
         // (prefetching the weights under the K loop costs registers past the
@@ -624,8 +673,18 @@ template <int BM, int BN, int WGM, int WGN, int BKT, int MINW, bool AK, bool BKc
           int MAP = 0, bool ROWSIMD = false>
 static void launch_one(const GemmParams& p, hipStream_t st) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, BKT, MINW, AK, BKc, TAG, MODE, MAP, ROWSIMD>),
-                     dim3(tiles, 1, p.nbatch * p.nsplit), dim3(64 * WGM * WGN), 0, st, p);
+  const dim3 grid(tiles, 1, p.nbatch * p.nsplit), blk(64 * WGM * WGN);
+  // the fused modes and ragged K under several reduce indices stage every tile masked (the
+  // latter under the untagged symbol: one masked instantiation per layout, not per call site)
+  if (MODE != 0)
+    hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, BKT, MINW, AK, BKc, TAG, MODE, MAP, ROWSIMD, true>), grid, blk,
+                       0, st, p);
+  else if (p.R > 1 && p.K % BKT != 0)
+    hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, BKT, MINW, AK, BKc, 0, 0, MAP, ROWSIMD, true>), grid, blk, 0,
+                       st, p);
+  else
+    hipLaunchKernelGGL((dgemm_kernel<BM, BN, WGM, WGN, BKT, MINW, AK, BKc, TAG, MODE, MAP, ROWSIMD, false>), grid,
+                       blk, 0, st, p);
 }
 
 // Engine shapes measured and removed: mode 1 on 128-point grid tiles
@@ -816,13 +875,9 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
     if (d.M <= 64) launch_one<64, 64, 2, 4, 16, 4, false, true, 5, 2, 1>(p, st);
     else           launch_one<128, 64, 2, 4, 16, 4, false, true, 5, 2, 1>(p, st);
   } else switch (cfg) {
-    case 0: launch_cfg<128, 128, 2, 4, 32, 2>(p, st, akc, bkc, d.tag); break;
-    case 1: launch_cfg<128, 128, 2, 2, 16, 2>(p, st, akc, bkc, d.tag); break;
     case 2: launch_cfg<128, 64, 2, 2, 32, 1>(p, st, akc, bkc, d.tag); break;
     case 3: launch_cfg<64, 128, 2, 2, 32, 1>(p, st, akc, bkc, d.tag); break;
     case 5: launch_cfg<128, 128, 2, 4, 16, 4>(p, st, akc, bkc, d.tag); break;
-    case 6: launch_cfg<256, 128, 4, 2, 16, 2>(p, st, akc, bkc, d.tag); break;
-    case 7: launch_cfg<128, 64, 2, 4, 16, 4>(p, st, akc, bkc, d.tag); break;
     case 8: launch_cfg<128, 128, 4, 2, 16, 4, true>(p, st, akc, bkc, d.tag); break;
     default: launch_cfg<64, 64, 2, 2, 32, 2>(p, st, akc, bkc, d.tag); break;
   }

@@ -12,6 +12,20 @@
 
 namespace xt {
 
+// Buffer descriptor over a wave-uniform base (readfirstlane'd so the compiler can prove it:
+// cdna_hip_programming.md T20); loads through it take a 32-bit lane offset and a scalar one,
+// so no 64-bit address arithmetic runs on the VALU.  The range is 2 GB from the base.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const double* p) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+__device__ __forceinline__ double bld8(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+
 // Fused XC grid contractions (GEMM modes, xt_gemm.hip).  Spin-channel x trial
 // vector pairs xg < nx, virtual index a < V, grid point g.
 //  mode 1 "rho forward":  rows m = 16 xg + a_l, reduce index r = a-block (a = 16 r + a_l),
@@ -79,7 +93,8 @@ int skinny_gemm(int M, int N, int K, double alpha, const double* A, long lda, co
 // dedicated XC M-backward (xt_xcm.hip): accT[i][xg V + a] += sum_g PhiO[g][i] *
 // sum_c wv[g][xg][c] dPhiV_c[g][a], O <= 128; split over g through a workspace
 // the grid arrays it reads (PhiO, dPhiV, wv) must stay readable XC_GRID_SLACK rows past
-// the chunk's last point (finite, zero-filled slack after the last grid point)
+// the chunk's last point: PhiO / dPhiV finite there, wv ZERO there (the kernel does not
+// mask grid points past n)
 constexpr int XC_GRID_SLACK = 64;
 size_t xc_back_m_workspace_bytes(int O, int nx, int V, int n);
 int xc_back_m(int O, int nx, int V, int n, const double* PO, long ldp, const double* W, long wc, long wg,

@@ -26,6 +26,7 @@
 // Split over the grid (K) for occupancy: each split writes its own slab, reduced in a
 // fixed order (deterministic) and added to accT.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include "xt_internal.h"
 
 namespace xt {
@@ -139,25 +140,30 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
     const int p = min(tid + NT * e, L::R - 1), gl = p / (3 * BM_XB), xc = p % (3 * BM_XB);
     orr[e] = (unsigned)(((long)gl * rg + 3 * min(x0 + xc / 3, nx - 1) + xc % 3) * 8);
   }
-  auto ld8 = [](const double* base, unsigned off) XT_INLINE {
-    return *(const double*)((const char*)base + off);
-  };
+  // Loads through buffer descriptors rebased per K-tile on wave-uniform (scalar) row
+  // pointers: the per-element offsets above are the only lane-varying part, so the
+  // staging runs no 64-bit address arithmetic on the VALU (whose issue cycles the FP64
+  // matrix pipe pays, tools/mfma_probe2.hip)
   auto load = [&](int kt) XT_INLINE {
-    const int g0 = kt * BM_BK;
-    const double* pa = PO + (long)g0 * ldp;
-    const double* pr = R + (long)g0 * rg;
+    const long g0 = (long)kt * BM_BK;
+    const __amdgpu_buffer_rsrc_t pa = rsrc_of(PO + g0 * ldp), pr = rsrc_of(R + g0 * rg);
+    const __amdgpu_buffer_rsrc_t pw[3] = {rsrc_of(Wg + g0 * wg), rsrc_of(Wg + wc + g0 * wg),
+                                          rsrc_of(Wg + 2 * wc + g0 * wg)};
 #pragma unroll
-    for (int e = 0; e < A_LD; ++e) ra[e] = ld8(pa, oa[e]);
+    for (int e = 0; e < A_LD; ++e) ra[e] = bld8(pa, oa[e], 0);
 #pragma unroll
-    for (int e = 0; e < W_LD; ++e) rw[e] = ld8(Wg + (e / 2) * wc + (long)g0 * wg, ow[e]);
+    for (int e = 0; e < W_LD; ++e) rw[e] = bld8(pw[e / 2], ow[e], 0);
 #pragma unroll
-    for (int e = 0; e < R_LD; ++e) rr[e] = ld8(pr, orr[e]);
+    for (int e = 0; e < R_LD; ++e) rr[e] = bld8(pr, orr[e], 0);
   };
-  // zeros make the padding inert: grid points past n (R = 0 -> B = 0), virtuals
-  // past V and pairs past nx (their columns are never stored; zero keeps them finite)
-  auto store = [&](int buf, int kt) XT_INLINE {
-    double* s = sm + buf * L::BUF;
-    const int g0 = kt * BM_BK;
+  // Padding: virtuals past V and pairs past nx read clamped (finite) columns and feed only
+  // accumulator columns / waves that are never stored.  Grid points past n read R's zeroed
+  // slack rows (xc_back_m's contract), so their B rows are zero.  LDS addresses are a
+  // per-thread base plus a compile-time offset (BUF is a template constant: the K loop is
+  // unrolled over the two buffers).
+  auto store = [&](auto BUF, int kt) XT_INLINE {
+    constexpr int B = decltype(BUF)::value;
+    double* s = sm + B * L::BUF;
 #pragma unroll
     for (int e = 0; e < A_LD; ++e) {
       const int p = tid + NT * e, gl = p / PA, i = p % PA;
@@ -166,16 +172,12 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
 #pragma unroll
     for (int e = 0; e < W_LD; ++e) {
       const int p = tid + NT * e, c = p / (BM_BK * BM_AB), gl = (p / BM_AB) % BM_BK, al = p % BM_AB;
-      s[L::A + (c * BM_BK + gl) * BM_AB + (al ^ ((gl & 1) << 4))] = a0 + al < V ? rw[e] : 0.0;
+      s[L::A + (c * BM_BK + gl) * BM_AB + (al ^ ((gl & 1) << 4))] = rw[e];
     }
+    (void)kt;
 #pragma unroll
-    for (int e = 0; e < R_LD; ++e) {
-      const int p = tid + NT * e;
-      if (p < L::R) {
-        const int gl = p / (3 * BM_XB), xc = p % (3 * BM_XB);
-        s[L::A + L::W + p] = (g0 + gl < n && x0 + xc / 3 < nx) ? rr[e] : 0.0;
-      }
-    }
+    for (int e = 0; e < R_LD; ++e)
+      if (tid + NT * e < L::R) s[L::A + L::W + tid + NT * e] = rr[e];
   };
 
   constexpr int TMM = RV ? TM - 1 : TM;        // MFMA row sub-tiles
@@ -200,8 +202,8 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
   const int a_lane = q * PA + ((r16) ^ ((q & 1) * SWA));        // A: row q, column r16 (+16 t via XOR-free add)
   const int w_lane = L::A + q * BM_AB;                           // W: row q
   const int r_lane = L::A + L::W + q * (3 * BM_XB) + 3 * wave;   // R: row q, this wave's pair
-  auto compute = [&](int buf) XT_INLINE {
-    const double* s = sm + buf * L::BUF;
+  auto compute = [&](auto BUF) XT_INLINE {
+    const double* s = sm + decltype(BUF)::value * L::BUF;
     auto gen = [&](int ks, double* b) XT_INLINE {
       const double* rrow = s + r_lane + 4 * ks * (3 * BM_XB);
       const double w0 = rrow[0], w1 = rrow[1], w2 = rrow[2];
@@ -251,18 +253,26 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
     // buffer was last read by K-tile kt - 1) and kt + 2 is loaded right after: the
     // stores overlap the other waves' MFMAs instead of delaying the barrier (writing
     // them before the closing barrier instead: +1 %)
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
     load(kt0);
-    store(0, kt0);
+    store(B0{}, kt0);
     if (kt0 + 1 < kt1) load(kt0 + 1);
     __syncthreads();
-    int buf = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      if (kt + 1 < kt1) store(buf ^ 1, kt + 1);
+    // one K-tile from buffer BUF (kt + 1 is staged into the other one)
+    auto tile = [&](auto BUF, int kt) XT_INLINE {
+      constexpr int B = decltype(BUF)::value;
+      if (kt + 1 < kt1) store(std::integral_constant<int, B ^ 1>{}, kt + 1);
       if (kt + 2 < kt1) load(kt + 2);
-      if (wave_on) compute(buf);
+      if (wave_on) compute(BUF);
       __syncthreads();
-      buf ^= 1;
+    };
+    int kt = kt0;
+    for (; kt + 2 <= kt1; kt += 2) {
+      tile(B0{}, kt);
+      tile(B1{}, kt + 1);
     }
+    if (kt < kt1) tile(B0{}, kt);
   }
   if (!wave_on) return;
   // C/D layout: col = lane & 15, row = q + 4 reg

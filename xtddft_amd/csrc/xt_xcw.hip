@@ -73,20 +73,6 @@ __device__ __forceinline__ double rows4(double v) {
   return pair(pair(v, false), true);
 }
 
-// buffer descriptor over a wave-uniform base (readfirstlane'd so the compiler can prove it:
-// cdna_hip_programming.md T20); loads through it take a 32-bit lane offset and a scalar one,
-// so no 64-bit address arithmetic runs on the VALU
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const double* p) {
-  const unsigned long long a = (unsigned long long)p;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, 0x7fffffff,
-                                           0x00020000);
-}
-__device__ __forceinline__ double bld8(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
-}
-
 // PB trial pairs per block (8, 4, 2, 1; Davidson steps with few new vectors): the
 // H = 8 / PB waves of a pair split each a-tile's k-step pairs into H even ranges,
 // contract their partial T with the same staged weights (the contraction is linear in T)

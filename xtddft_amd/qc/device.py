@@ -51,6 +51,18 @@ class DeviceEngine:
         self.naux = b.shape[0]
         self.B = b.to(self.dev).contiguous() if isinstance(b, torch.Tensor) else \
             torch.as_tensor(np.ascontiguousarray(b), device=self.dev)                    # (P, m, l)
+        # range-separated hybrids: the long-range factor of the same route (K_LR only)
+        self.B_lr = None
+        if getattr(mf, "omega", 0.0) != 0:
+            if mf.with_df is not None:
+                bl = np.asarray(mf.with_df.cderi_lr(mf.omega))
+            elif getattr(mf, "cderi_exact_lr", None) is not None:
+                bl = mf.cderi_exact_lr
+            else:
+                from .scf import pivoted_cholesky
+                bl = pivoted_cholesky(mf.eri_lr.reshape(n * n, n * n), 1e-14).reshape(-1, n, n)
+            self.B_lr = bl.to(self.dev).contiguous() if isinstance(bl, torch.Tensor) else \
+                torch.as_tensor(np.ascontiguousarray(bl), device=self.dev)
         if mf.xctype != "HF":
             ao = mf.ao
             self.ao = ao.to(self.dev) if isinstance(ao, torch.Tensor) else \
@@ -89,10 +101,21 @@ class DeviceEngine:
             vk = np.stack([self._k(d.reshape(-1, n, n)[x], dt[x]) for x in range(dt.shape[0])]).reshape(shape)
         return vj, vk
 
-    def _k(self, dh, dd):
+    def get_k(self, dms, lr=False):
+        """K[D] (lr: the long-range K_LR[D]) for each density of dms."""
+        d = np.asarray(dms, dtype=np.float64)
+        dt = self.torch.as_tensor(np.ascontiguousarray(d.reshape(-1, self.n, self.n)), device=self.dev)
+        B = self.B_lr if lr else self.B
+        if B is None:
+            raise ValueError("no long-range factor: the functional is not range-separated")
+        return np.stack([self._k(d.reshape(-1, self.n, self.n)[x], dt[x], B) for x in range(dt.shape[0])]
+                        ).reshape(d.shape)
+
+    def _k(self, dh, dd, B=None):
         """K[D] (host array) for one density (dh host, dd the same on the device)."""
         torch = self.torch
-        n, P = self.n, self.naux
+        B = self.B if B is None else B
+        n, P = self.n, B.shape[0]
         if np.abs(dh - dh.T).max() <= 1e-14 * max(1.0, np.abs(dh).max()):
             lam, v = np.linalg.eigh(0.5 * (dh + dh.T))
             keep = np.abs(lam) > 1e-14 * max(1.0, np.abs(lam).max())
@@ -100,11 +123,11 @@ class DeviceEngine:
             if r == 0:
                 return np.zeros((n, n))
             vt = torch.as_tensor(np.ascontiguousarray(v[:, keep]), device=self.dev)
-            t = self._mm(self.B.reshape(P * n, n), vt).reshape(P, n, r).permute(1, 0, 2).contiguous()
+            t = self._mm(B.reshape(P * n, n), vt).reshape(P, n, r).permute(1, 0, 2).contiguous()
             ts = t * torch.as_tensor(lam[keep], device=self.dev)
             return self._mm(t.reshape(n, P * r), ts.reshape(n, P * r), tb=1).cpu().numpy()
-        t = self._mm(self.B.reshape(P * n, n), dd).reshape(P, n, n).permute(1, 0, 2).contiguous()
-        return self._mm(t.reshape(n, P * n), self.B.reshape(P * n, n)).cpu().numpy()
+        t = self._mm(B.reshape(P * n, n), dd).reshape(P, n, n).permute(1, 0, 2).contiguous()
+        return self._mm(t.reshape(n, P * n), B.reshape(P * n, n)).cpu().numpy()
 
     # ------------------------------------------------------------ XC
     def _rho(self, dm):

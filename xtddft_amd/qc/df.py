@@ -98,6 +98,7 @@ class DF:
         self.device = device            # GPU for the 3-index integrals (None: host)
         self.auxmol = None
         self._cderi = None
+        self._cderi_lr = {}
 
     def build(self):
         if self._cderi is None:
@@ -114,20 +115,23 @@ class DF:
     def cderi_lr(self, omega: float):
         """The long-range factor of erf(omega r12)/r12 (PySCF ``with_df.range_coulomb``:
         3-index and 2-index integrals both attenuated), the ``cderi_lr`` of a
-        range-separated mean field (MeanField, XTDA.py:527-539).
-
-        A standalone integral capability: no range-separated functional is built
-        (``xc.rsh_and_hybrid_coeff`` returns omega = 0 for every functional here), so
-        ``_meanfield`` never fills ``cderi_lr`` and the operator's long-range exchange
-        (``operator.py``) is driven only by callers that supply the factor; its
-        end-to-end parity is unpinned."""
+        range-separated mean field (MeanField, XTDA.py:527-539): the SCF's long-range
+        exchange of CAM-B3LYP (``xc._RSH``) and the factor ``_meanfield`` hands the
+        operator.  Cached per omega."""
         self.build()
-        j3 = self.mol.int3c2e(self.auxmol, device=self.device, omega=omega)
-        return cholesky_cderi(j3, self.auxmol.int2c2e(omega=omega))
+        key = float(omega)
+        if key not in self._cderi_lr:
+            j3 = self.mol.int3c2e(self.auxmol, device=self.device, omega=omega)
+            self._cderi_lr[key] = cholesky_cderi(j3, self.auxmol.int2c2e(omega=omega))
+        return self._cderi_lr[key]
 
-    def get_jk(self, dms, with_j=True, with_k=True):
+    def get_k_lr(self, dms, omega: float):
+        """Long-range K[D] = sum_P L_P D L_P with the erf(omega r12)/r12 factor."""
+        return self.get_jk(dms, with_j=False, factor=self.cderi_lr(omega))[1]
+
+    def get_jk(self, dms, with_j=True, with_k=True, factor=None):
         """J[D] = sum_P B_P <B_P, D>, K[D] = sum_P B_P D B_P (PySCF convention)."""
-        b = self.cderi
+        b = self.cderi if factor is None else factor
         naux, n, _ = b.shape
         d = np.asarray(dms, dtype=np.float64)
         shape = d.shape

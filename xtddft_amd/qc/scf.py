@@ -13,7 +13,10 @@ Conventions kept from PySCF because the TDA operators read them:
   shells by alpha energy) or, with ``irrep_nelec = {irrep: (n_a, n_b)}``, the
   same rule inside each C2v irrep (``mol.ao_irreps``).
 * Energy pieces as PySCF prints them: E1 = sum_s tr(D_s h), Ecoul =
-  tr(D J)/2, Exc = E_xc[DFT] - hyb/2 sum_s tr(D_s K_s) (``uks.get_veff``).
+  tr(D J)/2, Exc = E_xc[DFT] - hyb/2 sum_s tr(D_s K_s) (``uks.get_veff``); a
+  range-separated hybrid (CAM-B3LYP) adds (alpha - hyb) K_LR[D] to hyb K[D], K_LR
+  from the erf(omega r12)/r12 ERIs of the same route (stored, DF or the device
+  Cholesky factor), as ``rks.get_veff`` does with ``get_k(omega=omega)``.
 
 Convergence: Pulay DIIS on (effective) Fock matrices, stop when |dE| <
 ``conv_tol`` and the orbital-rotation gradient norm < ``conv_tol_grad``.
@@ -54,6 +57,8 @@ class _SCFBase:
         self.eri_mode = "auto"          # 'incore' | 'cholesky' | 'auto' (see build)
         self.chol_tol = 1e-12
         self.cderi_exact = None
+        self.cderi_exact_lr = None
+        self.eri_lr = None
         self.timings = {}
         self.device_engine = None
         self._device = None
@@ -105,23 +110,31 @@ class _SCFBase:
         mol = self.mol
         dev = getattr(self, "_device", None)
         self.comps, self.hyb, self.xctype = _xc.parse_xc(self.xc)
+        self.omega, self.alpha = _xc.rsh_and_hybrid_coeff(self.xc)[:2] if self.xctype != "HF" else (0.0, 1.0)
         t0 = time.perf_counter()
         self.s1e = mol.intor("int1e_ovlp")
         self.h1e = mol.intor("int1e_kin") + mol.intor("int1e_nuc", device=dev)
         self.timings["int1e_s"] = time.perf_counter() - t0
-        self.eri = None
-        self._eri_k = None
-        self.cderi_exact = None
+        self.eri = self.eri_lr = None
+        self._eri_k = self._eri_k_lr = None
+        self.cderi_exact = self.cderi_exact_lr = None
         t0 = time.perf_counter()
+        rsh = self.omega != 0
         if self._use_cholesky():
             from .dchol import cholesky_eri
             st = {}
             self.cderi_exact = cholesky_eri(mol, self.chol_tol, dev, stats=st)
             self.timings["cholesky"] = st
+            if rsh:
+                self.cderi_exact_lr = cholesky_eri(mol, self.chol_tol, dev, omega=self.omega)
         elif self.with_df is None:
             self.eri = mol.eri_full(device=dev)
+            if rsh:
+                self.eri_lr = mol.eri_full(device=dev, omega=self.omega)
         else:
             self.with_df.build()
+            if rsh:
+                self.with_df.cderi_lr(self.omega)
         self.timings["int2e_s"] = time.perf_counter() - t0
         if self.xctype != "HF":
             t0 = time.perf_counter()
@@ -175,6 +188,22 @@ class _SCFBase:
                 self._eri_k = np.ascontiguousarray(self.eri.transpose(0, 3, 1, 2)).reshape(n * n, n * n)
             vk = (self._eri_k @ d.T).T.reshape(shape)
         return vj, vk
+
+    def get_k_lr(self, dm):
+        """Long-range exchange K_LR[D] with the erf(omega r12)/r12 operator
+        (``mf.get_k(mol, dm, hermi, omega=omega)``, XTDA.py:534-539)."""
+        if self.omega == 0:
+            raise ValueError(f"{self.xc} is not range-separated")
+        if self.device_engine is not None:
+            return self.device_engine.get_k(dm, lr=True)
+        if self.with_df is not None:
+            return self.with_df.get_k_lr(dm, self.omega)
+        d = np.asarray(dm, dtype=np.float64)
+        shape = d.shape
+        n = shape[-1]
+        if self._eri_k_lr is None:
+            self._eri_k_lr = np.ascontiguousarray(self.eri_lr.transpose(0, 3, 1, 2)).reshape(n * n, n * n)
+        return (self._eri_k_lr @ d.reshape(-1, n * n).T).T.reshape(shape)
 
     def _rho(self, dm):
         """rho (4, ngrid) (or (1, ngrid); MGGA (5, ngrid) with tau = 1/2 sum_c
@@ -232,7 +261,11 @@ class _SCFBase:
         else:
             exc, vxc = self._vxc(dms)
             veff = vxc + vj[None]
-            if self.hyb != 0:
+            if self.omega != 0:     # hyb K + (alpha - hyb) K_LR (XTDA.py:537-539)
+                vk = self.hyb * vk + (self.alpha - self.hyb) * self.get_k_lr(dms)
+                veff = veff - vk
+                exc -= 0.5 * (np.sum(dms[0] * vk[0]) + np.sum(dms[1] * vk[1]))
+            elif self.hyb != 0:
                 veff = veff - self.hyb * vk
                 exc -= 0.5 * self.hyb * (np.sum(dms[0] * vk[0]) + np.sum(dms[1] * vk[1]))
         ecoul = 0.5 * np.sum((dms[0] + dms[1]) * vj)
@@ -572,17 +605,24 @@ def _meanfield(mf, chol_tol):
     mol = mf.mol
     nao = mol.nao
     dms = mf._dm
+    omega, alpha, hyb = (0.0, 0.0, 1.0) if mf.xctype == "HF" else _xc.rsh_and_hybrid_coeff(mf.xc)
+    eri8_lr = cderi_lr = None
     if mf.with_df is not None:      # DF mean field: the fitted factor, no 4-index ERIs
         eri8 = None
         cderi = mf.with_df.cderi
+        if omega != 0:
+            cderi_lr = mf.with_df.cderi_lr(omega)
     elif mf.cderi_exact is not None:   # integral-direct Cholesky: the exact factor, on the device
         eri8 = None
         cderi = mf.cderi_exact
+        cderi_lr = mf.cderi_exact_lr
     else:
         eri8 = pack_s8(mf.eri)
         cderi = pivoted_cholesky(mf.eri.reshape(nao * nao, nao * nao), chol_tol).reshape(-1, nao, nao)
+        if omega != 0:
+            eri8_lr = pack_s8(mf.eri_lr)
+            cderi_lr = pivoted_cholesky(mf.eri_lr.reshape(nao * nao, nao * nao), chol_tol).reshape(-1, nao, nao)
     veff_hf = mf.get_veff_hf(dms)
-    omega, alpha, hyb = (0.0, 0.0, 1.0) if mf.xctype == "HF" else _xc.rsh_and_hybrid_coeff(mf.xc)
     grids = fxc = fxc_sf = None
     if mf.xctype != "HF":
         ao = mf.ao
@@ -603,7 +643,7 @@ def _meanfield(mf, chol_tol):
                     h1e=mf.h1e, veff=np.asarray(mf._veff), veff_hf=np.asarray(veff_hf),
                     cderi=cderi, grids=grids, fxc=fxc, fxc_sf=fxc_sf, xc=mf.xc,
                     xctype=mf.xctype, omega=omega, alpha=alpha, hyb=hyb, eri=eri8,
-                    e_tot=mf.e_tot)
+                    cderi_lr=cderi_lr, eri_lr=eri8_lr, e_tot=mf.e_tot)
     out.extra.update(dict(s1e=mf.s1e, orbsym=getattr(mf, "orbsym", None), qc_mol=mol))
     if not mf.restricted_open:
         out.extra["spin_square"] = mf.spin_square()

@@ -30,6 +30,22 @@ with tau = 1/2 sum |grad phi|^2 (no Laplacian):
 * TPSS correlation  revPKZB (eqs. 11-14) on PBE correlation (PRL 77, 3865 (1996)) over
                     PW92 (libxc's PW_MOD parameters), d = 2.8 Ha^-1
 
+Range separation (the reference's RSH branches: ``rsh_and_hybrid_coeff``, XTDA.py:82, 501;
+long-range K at XTDA.py:150-151, 527-539):
+
+* ITYH short-range B88 exchange  Iikura, Tsuneda, Yanai, Hirao, JCP 115, 3540 (2001):
+                    per spin e = -C_x rho_s^(4/3) F_B88(x_s) att(a_s), a_s = omega / (2 k_s),
+                    k_s = sqrt(9 pi / K_s) rho_s^(1/3), K_s = 2 C_x F_B88(x_s) (libxc GGA_X_ITYH
+                    with the B88 enhancement), att(a) = 1 - 8/3 a [sqrt(pi) erf(1/(2a))
+                    + (2a - 4a^3) exp(-1/(4a^2)) - 3a + 4a^3] (libxc attenuation_erf), its
+                    large-a series past a = 0.6 (the closed form cancels there)
+* CAM-B3LYP         libxc HYB_GGA_XC_CAM_B3LYP: 0.35 B88 + 0.46 ITYH-B88(omega) + 0.19 VWN5
+                    + 0.81 LYP, omega = 0.33, HF exchange 0.19 short-range + 0.65 long-range:
+                    PySCF's (omega, alpha, hyb) = (0.33, 0.65, 0.19), K = hyb K + (alpha - hyb) K_LR.
+                    Parity unpinned (no reference printout); checked by att's limits (omega -> 0
+                    gives B88, omega -> inf gives zero), the series / closed-form match, and the
+                    SCF's energy stationarity (tests/test_qc.py).
+
 TPSS = TPSS x + TPSS c, TPSSh = 0.1 HF + 0.9 TPSS x + TPSS c.  Pinned by two exact
 properties of the functional (tests/test_qc.py): the hydrogen-atom exchange energy is
 exactly -5/16 Ha and the correlation energy of any one-electron density is zero.
@@ -67,7 +83,10 @@ _FUNCTIONALS = {
     "B3LYP5": ([("slater", 0.08), ("b88", 0.72), ("vwn5", 0.19), ("lyp", 0.81)], 0.2, "GGA"),
     "TPSS": ([("tpss_x", 1.0), ("tpss_c", 1.0)], 0.0, "MGGA"),
     "TPSSH": ([("tpss_x", 0.9), ("tpss_c", 1.0)], 0.1, "MGGA"),
+    "CAMB3LYP": ([("b88", 0.35), ("ityh_b88@0.33", 0.46), ("vwn5", 0.19), ("lyp", 0.81)], 0.19, "GGA"),
 }
+# range-separated hybrids: name -> (omega, alpha) with PySCF's meaning (hyb from the table above)
+_RSH = {"CAMB3LYP": (0.33, 0.65)}
 NCOMP = {"HF": 1, "LDA": 1, "GGA": 4, "MGGA": 5}
 
 
@@ -80,9 +99,14 @@ def parse_xc(xc: str):
 
 
 def rsh_and_hybrid_coeff(xc: str):
-    """(omega, alpha, hyb) as PySCF returns them for a global hybrid
-    (the reference prints "Omega, alpha, hyb 0.0 0.5 0.5" for BHandHLYP)."""
+    """(omega, alpha, hyb) as PySCF returns them: (0, hyb, hyb) for a global hybrid (the
+    reference prints "Omega, alpha, hyb 0.0 0.5 0.5" for BHandHLYP); for a range-separated
+    hybrid K = hyb K + (alpha - hyb) K_LR(omega) (XTDA.py:537-539)."""
     _, hyb, _ = parse_xc(xc)
+    key = xc.upper().replace("-", "").replace(" ", "")
+    if key in _RSH:
+        omega, alpha = _RSH[key]
+        return omega, alpha, hyb
     return 0.0, hyb, hyb
 
 
@@ -263,6 +287,44 @@ def _tpss_c(ra, rb, saa, sab, sbb, ta, tb, torch):
     return n * e_rev * (1.0 + 2.8 * e_rev * zz * z)
 
 
+# attenuation of the erf-screened (short-range) LDA exchange hole, att(a) (libxc attenuation_erf)
+_ATT_SWITCH = 0.6
+_ATT_NSER = 24
+_ATT_C = [(-1.0) ** k * (2.0 / (math.factorial(k) * (2 * k + 1)) - 1.0 / math.factorial(k + 1)
+                         - 0.5 / math.factorial(k + 2)) for k in range(_ATT_NSER + 1)]
+
+
+def _att_erf(a, torch):
+    """1 - 8/3 a [sqrt(pi) erf(1/(2a)) + (2a - 4a^3) exp(-1/(4a^2)) - 3a + 4a^3].  Past a = 0.6
+    the bracket cancels to ~1/a: there the series att = -4/3 sum_k c_k u^k in u = 1/(4a^2)
+    (c_k from the erf and exp series; c_1 = -1/12 gives the 1/(36 a^2) tail)."""
+    small = a < _ATT_SWITCH
+    ad = torch.where(small, a, torch.full_like(a, _ATT_SWITCH))
+    direct = 1.0 - 8.0 / 3.0 * ad * (math.sqrt(math.pi) * torch.erf(0.5 / ad)
+                                     + (2.0 * ad - 4.0 * ad ** 3) * torch.exp(-0.25 / (ad * ad))
+                                     - 3.0 * ad + 4.0 * ad ** 3)
+    as_ = torch.where(small, torch.full_like(a, _ATT_SWITCH), a)
+    u = 0.25 / (as_ * as_)
+    ser = 0.0
+    for k in range(_ATT_NSER, 0, -1):          # Horner in u
+        ser = (ser + _ATT_C[k]) * u
+    return torch.where(small, direct, -4.0 / 3.0 * ser)
+
+
+def _ityh_b88(ra, rb, saa, sab, sbb, torch, omega):
+    """Short-range B88 exchange of Iikura-Tsuneda-Yanai-Hirao (libxc GGA_X_ITYH)."""
+    beta = 0.0042
+    out = 0.0
+    for r, s in ((ra, saa), (rb, sbb)):
+        r13 = r ** (1.0 / 3.0)
+        r43 = r * r13
+        y = s / (r43 * r43)
+        fx = 1.0 + beta / _CX * y / (1.0 + 6.0 * beta * _x_asinh_x(y, torch))
+        k = torch.sqrt(9.0 * math.pi / (2.0 * _CX * fx)) * r13
+        out = out - _CX * r43 * fx * _att_erf(omega / (2.0 * k), torch)
+    return out
+
+
 _PIECES = {"slater": _slater, "b88": _b88, "lyp": _lyp, "vwn5": _vwn5, "vwn_rpa": _vwn_rpa}
 _MPIECES = {"tpss_x": _tpss_x, "tpss_c": _tpss_c}
 
@@ -270,7 +332,9 @@ _MPIECES = {"tpss_x": _tpss_x, "tpss_c": _tpss_c}
 def _energy_density(comps, ra, rb, saa, sab, sbb, ta, tb, torch):
     eps = 0.0
     for name, coef in comps:
-        if name in _MPIECES:
+        if name.startswith("ityh_b88@"):
+            eps = eps + coef * _ityh_b88(ra, rb, saa, sab, sbb, torch, float(name.split("@")[1]))
+        elif name in _MPIECES:
             eps = eps + coef * _MPIECES[name](ra, rb, saa, sab, sbb, ta, tb, torch)
         else:
             eps = eps + coef * _PIECES[name](ra, rb, saa, sab, sbb, torch)
