@@ -57,6 +57,16 @@ class Grid:
         return int(self.ao.shape[0])
 
 
+def _pad_rows(b, n):
+    """b (naux, nao, nao) with zero rows appended up to n (NumPy or a torch tensor)."""
+    if int(b.shape[0]) == n:
+        return b
+    if type(b).__module__.startswith("torch"):
+        import torch
+        return torch.cat([b, b.new_zeros((n - b.shape[0],) + tuple(b.shape[1:]))])
+    return np.concatenate([np.asarray(b), np.zeros((n - b.shape[0],) + b.shape[1:])])
+
+
 @dataclass
 class MeanField:
     """``mf`` duck type (ROKS when ``mo_coeff.ndim == 2``, UKS when 3).
@@ -130,6 +140,13 @@ class MeanField:
             raise ValueError("need a DF factor (cderi) or stored ERIs (eri)")
         if self.cderi is not None and (self.cderi.ndim != 3 or self.cderi.shape[1:] != (self.nao, self.nao)):
             raise ValueError("cderi must be (naux, nao, nao)")
+        if self.cderi is not None and self.cderi_lr is not None:
+            if self.cderi_lr.ndim != 3 or tuple(self.cderi_lr.shape[1:]) != (self.nao, self.nao):
+                raise ValueError("cderi_lr must be (naux_lr, nao, nao)")
+            # the operator streams both factors over one aux window: a common row count,
+            # zero rows padding the shorter factor (they add nothing to J or K)
+            n = max(int(self.cderi.shape[0]), int(self.cderi_lr.shape[0]))
+            self.cderi, self.cderi_lr = _pad_rows(self.cderi, n), _pad_rows(self.cderi_lr, n)
         npair = self.nao * (self.nao + 1) // 2
         for name in ("eri", "eri_lr"):
             e = getattr(self, name)
