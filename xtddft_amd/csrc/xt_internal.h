@@ -96,6 +96,35 @@ int skinny_gemm(int M, int N, int K, double alpha, const double* A, long lda, co
 // the chunk's last point: PhiO / dPhiV finite there, wv ZERO there (the kernel does not
 // mask grid points past n)
 constexpr int XC_GRID_SLACK = 64;
+// Trial-pair segments for the dedicated XC kernels (Davidson steps with nx not a multiple
+// of 8): nx pairs covered by blocks of 8 / 4 / 2 / 1 pairs minimising the summed per-block
+// cost (cost[k]: a block of 8 >> k pairs); returns the segment count, segment s covering the
+// next cnt[s] pairs with blocks of pb[s] pairs, largest blocks first (one launch each)
+inline int xc_pair_segments(int nx, const double cost[4], int pb[4], int cnt[4]) {
+  if (nx <= 0) return 0;
+  double best[1025];
+  int pick[1025];
+  const int m_max = nx < 1024 ? nx : 1024;
+  best[0] = 0.0;
+  for (int m = 1; m <= m_max; ++m) {
+    best[m] = 1e300; pick[m] = 0;
+    for (int k = 0; k < 4; ++k) {
+      const int sz = 8 >> k, rest = m > sz ? m - sz : 0;
+      const double c = cost[k] + best[rest];
+      if (c < best[m] - 1e-12) { best[m] = c; pick[m] = k; }
+    }
+  }
+  int pairs[4] = {nx - m_max, 0, 0, 0};   // beyond 1024 pairs: 8-pair blocks
+  for (int m = m_max; m > 0;) {
+    const int k = pick[m], sz = 8 >> k;
+    pairs[k] += m < sz ? m : sz;
+    m = m > sz ? m - sz : 0;
+  }
+  int ns = 0;
+  for (int k = 0; k < 4; ++k)
+    if (pairs[k] > 0) { pb[ns] = 8 >> k; cnt[ns] = pairs[k]; ++ns; }
+  return ns;
+}
 size_t xc_back_m_workspace_bytes(int O, int nx, int V, int n);
 int xc_back_m(int O, int nx, int V, int n, const double* PO, long ldp, const double* W, long wc, long wg,
               const double* R, long rg, double* C, long ldc, double* ws, size_t ws_bytes, hipStream_t st);

@@ -33,6 +33,7 @@ namespace xt {
 
 #define XT_INLINE __attribute__((always_inline))
 typedef double d4m __attribute__((ext_vector_type(4)));
+typedef double d2m __attribute__((ext_vector_type(2)));
 
 constexpr int BM_AB = 32;        // virtuals per block (2 MFMA column sub-tiles per wave)
 // Block shapes: NW waves (one trial pair each), K-tiles of 4 NW grid points, LDS ~15 NW KB
@@ -41,18 +42,28 @@ constexpr int BM_AB = 32;        // virtuals per block (2 MFMA column sub-tiles 
 //   NW 4 / 2 / 1: two / four / eight blocks per CU, for Davidson steps with few trial
 //   pairs (nx = 2 nz < 8 would leave most waves of an 8-wave block idle)
 
-// LDS images (doubles), one buffer:
-//   A  [g 32][i 16 TM]        swizzle i ^ 16 (g & 1) for even TM (odd TM: the row pitch
-//                             16 TM = 16 mod 32 doubles already separates the halves)
-//   W  [c 3][g 32][a 32]      swizzle a ^ 16 (g & 1)
-//   R  [g 32][xg 8][c 3]      (broadcast reads)
-template <int TM, int NW>
+// K-tile grid points of an NW-wave block: whole k-step pairs (8 points per pair)
+__host__ __device__ constexpr int bm_bk(int nw) { return nw >= 2 ? 4 * nw : 8; }
+
+// LDS images in 16-B slots, each holding one value at a POINT PAIR (g, g + 1): lane q of
+// k-step pair p supplies grid points 2 (4 p + q) + {0, 1} to k-steps 2 p and 2 p + 1 (the
+// same permutation of the sum over g in both operands), so one ds_read_b128 feeds two
+// k-steps and every read is a per-lane base plus a compile-time offset.  The two buffers
+// of an image sit side by side (offsets stay inside the 16-bit ds offset field).
+//   A  [pair][i < 16 TMM]         PhiO, the MFMA rows
+//   W  [c 3][pair][a 32]          gradient planes of the block's virtuals
+//   R  [pair][xg NW][c 3]         wv (broadcast reads)
+//   RM [pair][r 8]                PhiO remainder rows 16 TMM + r (broadcast; RV > 0)
+// Conflicts: ds_read_b128 serves 16-lane groups mixing two q rows, so each image's row
+// length is 0 mod 16 slots (A, W) or the two rows' broadcast slots differ mod 16 (R: 3 NW,
+// RM: 8); ds_write_b128 groups of 8 lanes write 8 consecutive slots.
+template <int TM, int RV, int NW>
 struct BmLds {
-  static constexpr int BK = 4 * NW, XB = NW;
-  static constexpr int A = BK * 16 * TM;
-  static constexpr int W = 3 * BK * BM_AB;
-  static constexpr int R = BK * XB * 3;
-  static constexpr int BUF = A + W + R;
+  static constexpr int TMM = RV ? TM - 1 : TM;
+  static constexpr int BK = bm_bk(NW), NPR = BK / 2, KP = BK / 8;
+  static constexpr int PI = 16 * TMM, PR = 3 * NW;
+  static constexpr int A = NPR * PI, W = 3 * NPR * BM_AB, R = NPR * PR, RM = RV ? NPR * 8 : 0;
+  static constexpr int OA = 0, OW = 2 * A, OR = OW + 2 * W, ORM = OR + 2 * R, TOTAL = ORM + 2 * RM;
 };
 
 // rows4: sum of v over the four 16-lane rows (lanes l, l^16, l^32, l^48), in every lane
@@ -79,14 +90,12 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
             const double* __restrict__ Wg, long wc, long wg,
             const double* __restrict__ R, long rg,
             double* __restrict__ out, long ldo, long slab) {
-  using L = BmLds<TM, NW>;
-  constexpr int BM_BK = L::BK, BM_XB = L::XB, NT = 64 * NW;
-  constexpr int R_LD = (L::R + NT - 1) / NT;
-  constexpr int PA = 16 * TM;                  // A row length (i)
-  constexpr int A_LD = BM_BK * PA / NT;        // = TM doubles per thread
-  constexpr int W_LD = 3 * BM_BK * BM_AB / NT;   // = 6
-  constexpr int SWA = TM % 2 == 0 ? 16 : 0;    // A-image swizzle (see BmLds)
-  __shared__ __attribute__((aligned(16))) double sm[2 * L::BUF];
+  using L = BmLds<TM, RV, NW>;
+  constexpr int TMM = L::TMM, BK = L::BK, KP = L::KP, PI = L::PI, PR = L::PR, NT = 64 * NW;
+  constexpr int A_PT = (L::A + NT - 1) / NT, W_PT = (L::W + NT - 1) / NT;
+  constexpr int R_PT = (L::R + NT - 1) / NT, M_PT = RV ? (L::RM + NT - 1) / NT : 0;
+  static_assert((L::NPR * BM_AB) % NT == 0, "a thread's W slots stay in one gradient plane");
+  __shared__ d2m smv[L::TOTAL];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -97,7 +106,7 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
   // contiguous range, ordered split-major, then a-tile, xg-tile fastest -- the
   // xg-tiles sharing one a-tile's gradient columns run side by side on one XCD
   // (its L2 serves the re-reads) and every block of a split reads the same PhiO rows.
-  const int ntx = (nx + BM_XB - 1) / BM_XB, nta = (V + BM_AB - 1) / BM_AB;
+  const int ntx = (nx + NW - 1) / NW, nta = (V + BM_AB - 1) / BM_AB;
   const int nblk = gridDim.x;
   int lid = blockIdx.x;
   {
@@ -107,80 +116,76 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
   const int xt = lid % ntx;
   const int at = (lid / ntx) % nta;
   const int split = lid / (ntx * nta);
-  const int x0 = xt * BM_XB, a0 = at * BM_AB;
-  const int nkt = (n + BM_BK - 1) / BM_BK;
+  const int x0 = xt * NW, a0 = at * BM_AB;
+  const int nkt = (n + BK - 1) / BK;
   const int kt0 = split * ktiles_per_split;
   const int kt1 = min(kt0 + ktiles_per_split, nkt);
   const int xg = x0 + wave;                    // this wave's trial pair
   const bool wave_on = xg < nx;
 
-  // ---- staging maps (per thread, fixed) -------------------------------------
-  // A: element e -> (g = (tid + 512 e) / PA, i = (tid + 512 e) % PA): 16-lane runs of
-  //    consecutive i (one 128-B global segment, one conflict-free ds_write_b64 group)
-  // W: element e -> (c, g, a) with a fastest over 32
-  // R: element e -> (g, xg_l, c), 768 values, threads 0..255 load a second one
-  double ra[A_LD], rw[W_LD], rr[R_LD];
-  // per-thread byte offsets from the K-tile's (wave-uniform) row bases, columns
-  // clamped once here.  Rows past n of the last K-tile are read unclamped: the
-  // callers keep BM_BK rows of zeroed slack after the grid arrays (XC_GRID_SLACK),
-  // and those rows' wv are stored as zero, so they add nothing.
-  unsigned oa[A_LD], ow[W_LD], orr[R_LD];
+  // ---- staging: slot e of an image -> (point pair, column); a slot's two values come
+  // from grid rows 2 pair and 2 pair + 1 (the second through a scalar offset of one row).
+  // Columns past V / pairs past nx / occupied rows past O are clamped (finite values
+  // feeding accumulator columns, waves or rows that are never stored); grid points past
+  // n read the zeroed wv slack (xc_back_m's contract), so their B rows are zero.
+  unsigned oa[A_PT], ow[W_PT], orr[R_PT], om[M_PT > 0 ? M_PT : 1];
 #pragma unroll
-  for (int e = 0; e < A_LD; ++e) {
-    const int p = tid + NT * e, gl = p / PA, i = p % PA;
-    oa[e] = (unsigned)(((long)gl * ldp + min(i, O - 1)) * 8);
+  for (int e = 0; e < A_PT; ++e) {
+    const int sl = min(tid + NT * e, L::A - 1), pr = sl / PI, i = sl % PI;
+    oa[e] = (unsigned)(((long)2 * pr * ldp + min(i, O - 1)) * 8);
   }
 #pragma unroll
-  for (int e = 0; e < W_LD; ++e) {
-    const int p = tid + NT * e, gl = (p / BM_AB) % BM_BK, al = p % BM_AB;
-    ow[e] = (unsigned)(((long)gl * wg + min(a0 + al, V - 1)) * 8);
+  for (int e = 0; e < W_PT; ++e) {
+    const int sl = min(tid + NT * e, L::W - 1), pr = (sl / BM_AB) % L::NPR, al = sl % BM_AB;
+    ow[e] = (unsigned)(((long)2 * pr * wg + min(a0 + al, V - 1)) * 8);
   }
 #pragma unroll
-  for (int e = 0; e < R_LD; ++e) {
-    const int p = min(tid + NT * e, L::R - 1), gl = p / (3 * BM_XB), xc = p % (3 * BM_XB);
-    orr[e] = (unsigned)(((long)gl * rg + 3 * min(x0 + xc / 3, nx - 1) + xc % 3) * 8);
+  for (int e = 0; e < R_PT; ++e) {
+    const int sl = min(tid + NT * e, L::R - 1), pr = sl / PR, xc = sl % PR;
+    orr[e] = (unsigned)(((long)2 * pr * rg + 3 * min(x0 + xc / 3, nx - 1) + xc % 3) * 8);
   }
-  // Loads through buffer descriptors rebased per K-tile on wave-uniform (scalar) row
-  // pointers: the per-element offsets above are the only lane-varying part, so the
-  // staging runs no 64-bit address arithmetic on the VALU (whose issue cycles the FP64
-  // matrix pipe pays, tools/mfma_probe2.hip)
+#pragma unroll
+  for (int e = 0; e < M_PT; ++e) {
+    const int sl = min(tid + NT * e, L::RM - 1), pr = sl / 8, r = sl % 8;
+    om[e] = (unsigned)(((long)2 * pr * ldp + 16 * TMM + min(r, RV - 1)) * 8);
+  }
+  d2m ra[A_PT], rw[W_PT], rr[R_PT], rm_[M_PT > 0 ? M_PT : 1];
+  // loads through buffer descriptors rebased per K-tile on wave-uniform row pointers
+  // (no 64-bit address arithmetic on the VALU, whose issue cycles the FP64 matrix pipe pays)
   auto load = [&](int kt) XT_INLINE {
-    const long g0 = (long)kt * BM_BK;
+    const long g0 = (long)kt * BK;
     const __amdgpu_buffer_rsrc_t pa = rsrc_of(PO + g0 * ldp), pr = rsrc_of(R + g0 * rg);
     const __amdgpu_buffer_rsrc_t pw[3] = {rsrc_of(Wg + g0 * wg), rsrc_of(Wg + wc + g0 * wg),
                                           rsrc_of(Wg + 2 * wc + g0 * wg)};
+    const int sp = (int)(ldp * 8), sw = (int)(wg * 8), sr = (int)(rg * 8);
 #pragma unroll
-    for (int e = 0; e < A_LD; ++e) ra[e] = bld8(pa, oa[e], 0);
+    for (int e = 0; e < A_PT; ++e) ra[e] = (d2m){bld8(pa, oa[e], 0), bld8(pa, oa[e], sp)};
 #pragma unroll
-    for (int e = 0; e < W_LD; ++e) rw[e] = bld8(pw[e / 2], ow[e], 0);
+    for (int e = 0; e < W_PT; ++e) {
+      constexpr int WPC = L::NPR * BM_AB / NT;   // slots per thread and plane
+      rw[e] = (d2m){bld8(pw[e / WPC], ow[e], 0), bld8(pw[e / WPC], ow[e], sw)};
+    }
 #pragma unroll
-    for (int e = 0; e < R_LD; ++e) rr[e] = bld8(pr, orr[e], 0);
+    for (int e = 0; e < R_PT; ++e) rr[e] = (d2m){bld8(pr, orr[e], 0), bld8(pr, orr[e], sr)};
+#pragma unroll
+    for (int e = 0; e < M_PT; ++e) rm_[e] = (d2m){bld8(pa, om[e], 0), bld8(pa, om[e], sp)};
   };
-  // Padding: virtuals past V and pairs past nx read clamped (finite) columns and feed only
-  // accumulator columns / waves that are never stored.  Grid points past n read R's zeroed
-  // slack rows (xc_back_m's contract), so their B rows are zero.  LDS addresses are a
-  // per-thread base plus a compile-time offset (BUF is a template constant: the K loop is
-  // unrolled over the two buffers).
-  auto store = [&](auto BUF, int kt) XT_INLINE {
+  auto store = [&](auto BUF) XT_INLINE {
     constexpr int B = decltype(BUF)::value;
-    double* s = sm + B * L::BUF;
 #pragma unroll
-    for (int e = 0; e < A_LD; ++e) {
-      const int p = tid + NT * e, gl = p / PA, i = p % PA;
-      s[gl * PA + (i ^ ((gl & 1) * SWA))] = ra[e];
-    }
+    for (int e = 0; e < A_PT; ++e)
+      if (L::A % NT == 0 || tid + NT * e < L::A) smv[L::OA + B * L::A + tid + NT * e] = ra[e];
 #pragma unroll
-    for (int e = 0; e < W_LD; ++e) {
-      const int p = tid + NT * e, c = p / (BM_BK * BM_AB), gl = (p / BM_AB) % BM_BK, al = p % BM_AB;
-      s[L::A + (c * BM_BK + gl) * BM_AB + (al ^ ((gl & 1) << 4))] = rw[e];
-    }
-    (void)kt;
+    for (int e = 0; e < W_PT; ++e)
+      if (L::W % NT == 0 || tid + NT * e < L::W) smv[L::OW + B * L::W + tid + NT * e] = rw[e];
 #pragma unroll
-    for (int e = 0; e < R_LD; ++e)
-      if (tid + NT * e < L::R) s[L::A + L::W + tid + NT * e] = rr[e];
+    for (int e = 0; e < R_PT; ++e)
+      if (L::R % NT == 0 || tid + NT * e < L::R) smv[L::OR + B * L::R + tid + NT * e] = rr[e];
+#pragma unroll
+    for (int e = 0; e < M_PT; ++e)
+      if (L::RM % NT == 0 || tid + NT * e < L::RM) smv[L::ORM + B * L::RM + tid + NT * e] = rm_[e];
   };
 
-  constexpr int TMM = RV ? TM - 1 : TM;        // MFMA row sub-tiles
   constexpr int RVA = RV ? RV : 1;
   d4m acc[TMM > 0 ? TMM : 1][2];
 #pragma unroll
@@ -191,62 +196,60 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
 #pragma unroll
   for (int r = 0; r < RVA; ++r) part[r][0] = part[r][1] = 0.0;
 
-  // one K-tile: 8 k-steps; lane (q, r16) feeds k = g_l = 4 s + q.  Row parity of g_l
-  // is the parity of q, so the swizzles are per-lane constants and every LDS address
-  // below is a lane base plus a compile-time offset.
-  // The B fragments of k-step s + 1 are generated before the MFMAs of step s in
-  // program order (their LDS reads and the 3-deep FP64 chain then overlap step s's
-  // matrix work instead of stalling step s + 1's first MFMA; building all 8 steps'
-  // fragments up front measured +4 %).
-  const int swl = (q & 1) << 4;
-  const int a_lane = q * PA + ((r16) ^ ((q & 1) * SWA));        // A: row q, column r16 (+16 t via XOR-free add)
-  const int w_lane = L::A + q * BM_AB;                           // W: row q
-  const int r_lane = L::A + L::W + q * (3 * BM_XB) + 3 * wave;   // R: row q, this wave's pair
+  // one K-tile: KP k-step pairs.  The B fragments of pair p + 1 are generated before the
+  // MFMAs of pair p in program order (their LDS reads and the 3-deep FP64 chain overlap
+  // pair p's matrix work).
+  const int la = q * PI + r16, lw = q * BM_AB + r16, lr = q * PR + 3 * wave, lm = q * 8;
   auto compute = [&](auto BUF) XT_INLINE {
-    const double* s = sm + decltype(BUF)::value * L::BUF;
-    auto gen = [&](int ks, double* b) XT_INLINE {
-      const double* rrow = s + r_lane + 4 * ks * (3 * BM_XB);
-      const double w0 = rrow[0], w1 = rrow[1], w2 = rrow[2];
+    constexpr int B = decltype(BUF)::value;
+    const d2m* sA = smv + L::OA + B * L::A + la;
+    const d2m* sW = smv + L::OW + B * L::W + lw;
+    const d2m* sR = smv + L::OR + B * L::R + lr;
+    const d2m* sM = smv + L::ORM + B * L::RM + lm;
+    auto gen = [&](int p, double (*b)[2]) XT_INLINE {   // b[step][j]
+      const d2m w0 = sR[4 * p * PR], w1 = sR[4 * p * PR + 1], w2 = sR[4 * p * PR + 2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const double* wr = s + w_lane + 4 * ks * BM_AB + ((16 * j + r16) ^ swl);
-        b[j] = w0 * wr[0] + w1 * wr[BM_BK * BM_AB] + w2 * wr[2 * BM_BK * BM_AB];
+        const d2m g0 = sW[(4 * p) * BM_AB + 16 * j];
+        const d2m g1 = sW[(L::NPR + 4 * p) * BM_AB + 16 * j];
+        const d2m g2 = sW[(2 * L::NPR + 4 * p) * BM_AB + 16 * j];
+        b[0][j] = w0[0] * g0[0] + w1[0] * g1[0] + w2[0] * g2[0];
+        b[1][j] = w0[1] * g0[1] + w1[1] * g1[1] + w2[1] * g2[1];
       }
     };
-    auto mma = [&](int ks, const double* b) XT_INLINE {
-      double af[TMM > 0 ? TMM : 1];
+    auto mma = [&](int p, double (*b)[2]) XT_INLINE {
+      d2m af[TMM > 0 ? TMM : 1];
 #pragma unroll
-      for (int t = 0; t < TMM; ++t) {
-        // (16 t + r16) ^ sw = 16 (t ^ (sw / 16)) + r16: the swizzle permutes whole sub-tiles
-        const int tt = SWA ? (t ^ (q & 1)) : t;
-        af[t] = s[q * PA + 4 * ks * PA + 16 * tt + r16];
-      }
+      for (int t = 0; t < TMM; ++t) af[t] = sA[4 * p * PI + 16 * t];
+      d2m mr[RVA];
       if constexpr (RV > 0) {
-        // the remainder rows: phi_i(g) for i = 16 (TM - 1) + r, broadcast over the 16 lanes of a k-row
-        const int tl = SWA ? ((TM - 1) ^ (q & 1)) : TM - 1;
-        const double* rrw = s + q * PA + 4 * ks * PA + 16 * tl;
 #pragma unroll
-        for (int r = 0; r < RV; ++r) {
-          const double v = rrw[r];
-          part[r][0] += v * b[0];
-          part[r][1] += v * b[1];
-        }
+        for (int r = 0; r < RV; ++r) mr[r] = sM[4 * p * 8 + r];
       }
 #pragma unroll
-      for (int t = 0; t < TMM; ++t)
+      for (int st = 0; st < 2; ++st) {
+        if constexpr (RV > 0) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t], b[j], acc[t][j], 0, 0, 0);
+          for (int r = 0; r < RV; ++r) {
+            part[r][0] += mr[r][st] * b[st][0];
+            part[r][1] += mr[r][st] * b[st][1];
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < TMM; ++t)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t][st], b[st][j], acc[t][j], 0, 0, 0);
+      }
     };
-    double b[2][2];
+    double b[2][2][2];
     gen(0, b[0]);
 #pragma unroll
-    for (int ks = 0; ks < BM_BK / 4; ++ks) {
-      if (ks + 1 < BM_BK / 4) gen(ks + 1, b[(ks + 1) & 1]);
-      mma(ks, b[ks & 1]);
+    for (int p = 0; p < KP; ++p) {
+      if (p + 1 < KP) gen(p + 1, b[(p + 1) & 1]);
+      mma(p, b[p & 1]);
     }
   };
-  (void)a_lane;
 
   if (kt0 < kt1) {
     // K-tile kt + 1 is written to LDS right after the barrier that opens K-tile kt (its
@@ -256,13 +259,13 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, 1>;
     load(kt0);
-    store(B0{}, kt0);
+    store(B0{});
     if (kt0 + 1 < kt1) load(kt0 + 1);
     __syncthreads();
     // one K-tile from buffer BUF (kt + 1 is staged into the other one)
     auto tile = [&](auto BUF, int kt) XT_INLINE {
       constexpr int B = decltype(BUF)::value;
-      if (kt + 1 < kt1) store(std::integral_constant<int, B ^ 1>{}, kt + 1);
+      if (kt + 1 < kt1) store(std::integral_constant<int, B ^ 1>{});
       if (kt + 2 < kt1) load(kt + 2);
       if (wave_on) compute(BUF);
       __syncthreads();
@@ -295,7 +298,7 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const double v = rows4_m(part[r][j]);
-        const int i = 16 * (TM - 1) + r, a = a0 + 16 * j + r16;
+        const int i = 16 * TMM + r, a = a0 + 16 * j + r16;
         if (q == 0 && i < O && a < V) o[(long)i * ldo + (long)xg * V + a] = v;
       }
   }
@@ -329,27 +332,18 @@ static int back_m_splits(int tiles, int nkt, int slots) {
   return best;
 }
 
-// Block shape by the trial pairs: relative cost = blocks per a-tile x NW (the MFMA work)
-// x (1 + the shape's overhead): smaller K-tiles mean more barriers and more PhiO staging
-// per MFMA (per pair, relative to NW 8 at nx = 8: NW 4 +12 %, NW 2 +75 %)
-static int back_m_nw(int nx) {
-  const int nws[4] = {8, 4, 2, 1};
-  const double pen[4] = {0.0, 0.12, 0.75, 2.0};   // measured at the headline shape
-  int best = 8;
-  double best_cost = 1e30;
-  for (int k = 0; k < 4; ++k) {
-    const int nw = nws[k];
-    const double cost = (double)((nx + nw - 1) / nw) * nw * (1.0 + pen[k]);
-    if (cost < best_cost - 1e-9) { best_cost = cost; best = nw; }
-  }
-  return best;
-}
+// Block shapes by the trial pairs: relative cost of a block of NW = 8 / 4 / 2 / 1 pairs per
+// a-tile = NW (its MFMA work) x (1 + the shape's overhead) / 8: smaller K-tiles mean more
+// barriers and more PhiO / weight staging per MFMA (per pair, relative to NW 8 at nx = 8:
+// NW 4 +12 %, NW 2 +75 %, measured at the headline shape).  A step's nx pairs
+// are split into segments of one shape each (xc_pair_segments), e.g. 10 = 8 + 2.
+static const double kBackMCost[4] = {1.0, 4.0 * 1.12 / 8.0, 2.0 * 1.75 / 8.0, 1.0 * 3.0 / 8.0};
 
 struct BackMPlan { int nw, tiles, nkt, splits, kps, used, blocks; };
-static BackMPlan back_m_plan(int nx, int V, int n) {
+static BackMPlan back_m_plan(int nw, int nx, int V, int n) {
   BackMPlan p;
-  p.nw = back_m_nw(nx);
-  const int bk = 4 * p.nw, xb = p.nw;
+  p.nw = nw;
+  const int bk = bm_bk(p.nw), xb = p.nw;
   p.tiles = ((nx + xb - 1) / xb) * ((V + BM_AB - 1) / BM_AB);
   p.nkt = (n + bk - 1) / bk;
   p.splits = back_m_splits(p.tiles, p.nkt, 256 * (8 / p.nw));
@@ -360,8 +354,15 @@ static BackMPlan back_m_plan(int nx, int V, int n) {
 }
 
 size_t xc_back_m_workspace_bytes(int O, int nx, int V, int n) {
-  const BackMPlan p = back_m_plan(nx, V, n);
-  return sizeof(double) * (size_t)p.splits * O * (size_t)nx * V;
+  int pb[4], cnt[4];
+  const int ns = xc_pair_segments(nx, kBackMCost, pb, cnt);
+  size_t need = 0;
+  for (int s = 0; s < ns; ++s) {
+    const BackMPlan p = back_m_plan(pb[s], cnt[s], V, n);
+    const size_t b = sizeof(double) * (size_t)p.splits * O * (size_t)cnt[s] * V;
+    need = b > need ? b : need;
+  }
+  return need;
 }
 
 // remainder rows on the VALU for the occupied counts of the BASELINE shapes (O = 33..40:
@@ -399,20 +400,28 @@ int xc_back_m(int O, int nx, int V, int n, const double* PO, long ldp, const dou
               const double* R, long rg, double* C, long ldc, double* ws, size_t ws_bytes, hipStream_t st) {
   if (O <= 0 || nx <= 0 || V <= 0 || n <= 0) return 0;
   if (O > 128) return XT_ERR_ARG;                      // one row tile (the engine's mode 2 covers more)
-  const BackMPlan p = back_m_plan(nx, V, n);
-  const long slab = (long)O * nx * V;
-  if (ws_bytes < sizeof(double) * (size_t)p.splits * slab) return XT_ERR_ARG;
+  if (ws_bytes < xc_back_m_workspace_bytes(O, nx, V, n)) return XT_ERR_ARG;
   const int TM = (O + 15) / 16;
-  switch (p.nw) {
-    case 8: launch_back_m_tm<8>(TM, O, nx, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
-    case 4: launch_back_m_tm<4>(TM, O, nx, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
-    case 2: launch_back_m_tm<2>(TM, O, nx, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
-    default: launch_back_m_tm<1>(TM, O, nx, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, R, rg, ws, slab, st); break;
+  int pb[4], cnt[4];
+  const int ns = xc_pair_segments(nx, kBackMCost, pb, cnt);
+  // segment s: pairs [x0, x0 + cnt) -- its wv columns and accT columns, a workspace laid
+  // out for its own pairs, reduced into C's column window
+  for (int s = 0, x0 = 0; s < ns; x0 += cnt[s], ++s) {
+    const int nxs = cnt[s];
+    const BackMPlan p = back_m_plan(pb[s], nxs, V, n);
+    const long slab = (long)O * nxs * V;
+    const double* Rs = R + 3L * x0;
+    switch (p.nw) {
+      case 8: launch_back_m_tm<8>(TM, O, nxs, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, Rs, rg, ws, slab, st); break;
+      case 4: launch_back_m_tm<4>(TM, O, nxs, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, Rs, rg, ws, slab, st); break;
+      case 2: launch_back_m_tm<2>(TM, O, nxs, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, Rs, rg, ws, slab, st); break;
+      default: launch_back_m_tm<1>(TM, O, nxs, V, n, p.kps, p.blocks, PO, ldp, W, wc, wg, Rs, rg, ws, slab, st); break;
+    }
+    int rb = (int)((slab + 255) / 256);
+    if (rb > 8192) rb = 8192;
+    hipLaunchKernelGGL(k_xc_back_m_reduce, dim3(rb), dim3(256), 0, st, O, (long)nxs * V, p.used, ws, slab,
+                       C + (long)x0 * V, ldc);
   }
-  const long total = slab;
-  int rb = (int)((total + 255) / 256);
-  if (rb > 8192) rb = 8192;
-  hipLaunchKernelGGL(k_xc_back_m_reduce, dim3(rb), dim3(256), 0, st, O, (long)nx * V, p.used, ws, slab, C, ldc);
   return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
 }
 

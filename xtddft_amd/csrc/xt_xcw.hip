@@ -332,19 +332,12 @@ static void lds_attribute(K kern, int slot) {
   if (dev < 64) done[slot] |= 1ull << dev;
 }
 
-// pairs per block: relative block time ~ PB / 8 (the k-steps each wave runs) + 0.27 (the
-// per-a-tile contraction, staging and barrier; fitted to the nvec sweep of the VALU-free
-// kernel: a 4-pair block costs 0.60, a 2-pair block 0.415 of an 8-pair block), times the
-// blocks per grid tile; the cheapest wins
-static int rho_w_pb(int nx) {
-  int best = 8;
-  double best_cost = 1e30;
-  for (int pb = 8; pb >= 1; pb /= 2) {
-    const double cost = (double)((nx + pb - 1) / pb) * (pb / 8.0 + 0.27);
-    if (cost < best_cost - 1e-9) { best_cost = cost; best = pb; }
-  }
-  return best;
-}
+// Block shapes by the trial pairs: relative block time ~ PB / 8 (the k-steps each wave
+// runs) + 0.27 (the per-a-tile contraction, staging and barrier; fitted to the nvec sweep of
+// the VALU-free kernel: a 4-pair block costs 0.60, a 2-pair block 0.415 of an 8-pair block).
+// A step's nx pairs are split into segments of one shape each (xc_pair_segments, e.g.
+// 10 = 8 + 2 instead of three 4-pair blocks), one launch per segment.
+static const double kRhoWCost[4] = {1.0 + 0.27, 0.5 + 0.27, 0.25 + 0.27, 0.125 + 0.27};
 
 int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const double* Z, long zi, long zx,
              const double* W, long wc, long wg, double* R, long rg, hipStream_t st) {
@@ -352,16 +345,22 @@ int xc_rho_w(int O, int nx, int V, int n, const double* PO, long ldp, const doub
   const size_t lds = rho_w_lds(O);
   if (lds > 160 * 1024) return XT_ERR_ARG;
   const int ntg = (n + GB - 1) / GB;
-  const int pb = rho_w_pb(nx);
-  const int blocks = ntg * ((nx + pb - 1) / pb);
-#define XT_W(PBV, S)                                                                                       \
-  case PBV:                                                                                                \
-    lds_attribute(k_xc_rho_w<PBV>, S);                                                                     \
-    hipLaunchKernelGGL((k_xc_rho_w<PBV>), dim3(blocks), dim3(64 * WXB), lds, st, O, nx, V, n, PO, ldp, Z, \
-                       zi, zx, W, wc, wg, R, rg);                                                          \
+  int pbs[4], cnt[4];
+  const int ns = xc_pair_segments(nx, kRhoWCost, pbs, cnt);
+  for (int s = 0, x0 = 0; s < ns; x0 += cnt[s], ++s) {
+    const int nxs = cnt[s], pb = pbs[s];
+    const int blocks = ntg * ((nxs + pb - 1) / pb);
+    const double* Zs = Z + (long)x0 * zx;
+    double* Rs = R + 3L * x0;
+#define XT_W(PBV, S)                                                                                         \
+  case PBV:                                                                                                  \
+    lds_attribute(k_xc_rho_w<PBV>, S);                                                                       \
+    hipLaunchKernelGGL((k_xc_rho_w<PBV>), dim3(blocks), dim3(64 * WXB), lds, st, O, nxs, V, n, PO, ldp, Zs, \
+                       zi, zx, W, wc, wg, Rs, rg);                                                           \
     break;
-  switch (pb) { XT_W(8, 0) XT_W(4, 1) XT_W(2, 2) default: XT_W(1, 3) }
+    switch (pb) { XT_W(8, 0) XT_W(4, 1) XT_W(2, 2) default: XT_W(1, 3) }
 #undef XT_W
+  }
   return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
 }
 
