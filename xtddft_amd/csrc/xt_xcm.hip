@@ -217,15 +217,17 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
         b[1][j] = w0[1] * g0[1] + w1[1] * g1[1] + w2[1] * g2[1];
       }
     };
-    auto mma = [&](int p, double (*b)[2]) XT_INLINE {
-      d2m af[TMM > 0 ? TMM : 1];
+    d2m af[TMM > 0 ? TMM : 1], mr[RVA];
+    auto frag = [&](int p) XT_INLINE {          // pair p's A fragments and remainder values
 #pragma unroll
       for (int t = 0; t < TMM; ++t) af[t] = sA[4 * p * PI + 16 * t];
-      d2m mr[RVA];
       if constexpr (RV > 0) {
 #pragma unroll
         for (int r = 0; r < RV; ++r) mr[r] = sM[4 * p * 8 + r];
       }
+    };
+    auto mma = [&](int p, double (*b)[2]) XT_INLINE {
+      (void)p;
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         if constexpr (RV > 0) {
@@ -242,12 +244,28 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
             acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t][st], b[st][j], acc[t][j], 0, 0, 0);
       }
     };
+    // Per k-step pair, one scheduling region: all its LDS reads first (pair p's fragments,
+    // then pair p + 1's generator inputs), then the 2 TMM x 2 MFMAs of pair p with the
+    // FP64 VALU (pair p + 1's generation, pair p's remainder rows) interleaved between them
+    // -- left alone, the scheduler emitted read burst / wait / VALU burst / MFMA burst, so
+    // the LDS latency and the VALU were serialised with the matrix work.
+    constexpr int NMF = 2 * 2 * (TMM > 0 ? TMM : 1);
     double b[2][2][2];
     gen(0, b[0]);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int p = 0; p < KP; ++p) {
+      frag(p);
       if (p + 1 < KP) gen(p + 1, b[(p + 1) & 1]);
       mma(p, b[p & 1]);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);   // the first fragments
+#pragma unroll
+      for (int k = 0; k < NMF; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one DS read
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // up to two VALU
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
