@@ -816,16 +816,18 @@ static int build_kx(xt_ctx* c) {
       const DevBuf& B = pass ? c->Bmo_lr : c->Bmo;
       const double* Bo = bmo_full(c, B, gr[q].ob);   // all aux rows: Kx sums over every P
       const double* Bv = bmo_full(c, B, gr[q].vb) + (long)c->v0 * nmo + c->v0;
-      for (int i = i0; i < i1; ++i) {
-        // batch a: Kx[(i,a)][(j,b)] += coef sum_P Bo[P][i][j] Bv[P][a][b]
-        GemmDesc g;
-        g.M = O; g.N = V; g.K = naux; g.nb1 = V;
-        g.A = Bo + (long)i * nmo; g.sAm = 1; g.sAk = mm; g.sAb1 = 0;
-        g.B = Bv; g.sBk = mm; g.sBn = 1; g.sBb1 = nmo;
-        g.C = K + (size_t)i * V * ld; g.ldc = V; g.sCb1 = (long)ld;
-        g.alpha = coef; g.beta = 1.0;
-        RET(gemm(c, g));
-      }
+      // batch a: Kx[(i,a)][(j,b)] += coef sum_P Bo[P][i][j] Bv[P][a][b] with rows (i, j) of
+      // all this context's i in one GEMM (two-level rows: i strides nmo in Bo and V ld in
+      // Kx, j strides 1 and V) -- one launch of (i1 - i0) O rows instead of one per i,
+      // whose O = 101 rows filled 101 / 128 of a row tile
+      GemmDesc g;
+      g.M = (i1 - i0) * O; g.N = V; g.K = naux; g.nb1 = V;
+      g.rdiv = O; g.sAm_hi = nmo; g.sC_hi = (long)V * ld;
+      g.A = Bo + (long)i0 * nmo; g.sAm = 1; g.sAk = mm; g.sAb1 = 0;
+      g.B = Bv; g.sBk = mm; g.sBn = 1; g.sBb1 = nmo;
+      g.C = K + (size_t)i0 * V * ld; g.ldc = V; g.sCb1 = (long)ld;
+      g.alpha = coef; g.beta = 1.0;
+      RET(gemm(c, g));
     }
   }
   HIPCHK(hipStreamSynchronize(c->st));

@@ -173,7 +173,7 @@ dgemm_kernel(GemmParams p) {
   const long u1 = (u0 + u_per < units) ? (u0 + u_per) : units;
 
   const double* __restrict__ Ab = p.A + b1 * p.sAb1 + b2 * p.sAb2 +
-                                  (MODE == 1 ? 0L : (A_KC ? (long)m0 * p.sAm : (long)m0));
+                                  (MODE == 1 || p.rdiv ? 0L : (A_KC ? (long)m0 * p.sAm : (long)m0));
   const double* __restrict__ Bb = p.B + b1 * p.sBb1 + b2 * p.sBb2 +
                                   (B_KC ? (long)n0 * p.sBn : (long)n0);
 
@@ -192,6 +192,7 @@ dgemm_kernel(GemmParams p) {
   unsigned aoff[A_ELEMS], boff[B_ELEMS];
   // mode 1 rows m = 16 xg + a_l sit at xg * ablk + a_l (the a-block via r * sAr)
   auto rowoff = [&](int mg) XT_INLINE -> long {
+    if (MODE == 0 && !A_KC && p.rdiv) return (long)(mg / p.rdiv) * p.sAm_hi + mg % p.rdiv;
     return MODE == 1 ? (long)(mg >> 4) * p.fz.ablk + (mg & 15) : (long)(mg - m0);
   };
 #pragma unroll
@@ -617,7 +618,8 @@ dgemm_kernel(GemmParams p) {
           int gn = n0 + wn * WN + j * 16 + r16;
           const long cn = ccol(gn);
           if (gm < p.M && gn < p.N && cn >= 0) {
-            double* c = Cb + (long)gm * p.ldc + cn;
+            const long crow = p.rdiv ? (long)(gm / p.rdiv) * p.sC_hi + (long)(gm % p.rdiv) * p.ldc : (long)gm * p.ldc;
+            double* c = Cb + crow + cn;
             double v = p.alpha * acc[i][j][t];
             if (p.beta != 0.0) v += p.beta * (*c);
             *c = v;
@@ -645,7 +647,8 @@ __global__ void splitk_reduce(GemmParams p) {
     double s = 0.0;
     for (int sp = 0; sp < p.nsplit; ++sp) s += p.ws[((long)sp * p.nbatch + b) * mn + e];
     const int b1 = b / p.nb2, b2 = b % p.nb2;
-    double* c = p.C + b1 * p.sCb1 + b2 * p.sCb2 + (long)m * p.ldc + cn;
+    const long crow = p.rdiv ? (long)(m / p.rdiv) * p.sC_hi + (long)(m % p.rdiv) * p.ldc : (long)m * p.ldc;
+    double* c = p.C + b1 * p.sCb1 + b2 * p.sCb2 + crow + cn;
     double v = p.alpha * s;
     if (p.beta != 0.0) v += p.beta * (*c);
     *c = v;
@@ -792,6 +795,7 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
   p.A = d.A; p.sAm = d.sAm; p.sAk = d.sAk; p.sAr = d.sAr; p.sAb1 = d.sAb1; p.sAb2 = d.sAb2;
   p.B = d.B; p.sBk = d.sBk; p.sBn = d.sBn; p.sBr = d.sBr; p.sBb1 = d.sBb1; p.sBb2 = d.sBb2;
   p.C = d.C; p.ldc = d.ldc; p.sCb1 = d.sCb1; p.sCb2 = d.sCb2;
+  p.rdiv = d.rdiv; p.sAm_hi = d.sAm_hi; p.sC_hi = d.sC_hi;
   p.alpha = d.alpha; p.beta = d.beta;
   p.nb2 = d.nb2 > 0 ? d.nb2 : 1;
   p.nbatch = (d.nb1 > 0 ? d.nb1 : 1) * p.nb2;
@@ -845,11 +849,14 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
                     d.N != xc_m_cols(d.fz.nx, d.fz.V, d.fz.mbn))) return XT_ERR_ARG;
   const bool akc = mode == 0 && (d.sAk == 1);
   const bool bkc = mode != 0 || (d.sBk == 1);
+  if (d.rdiv < 0 || (d.rdiv > 0 && (mode != 0 || d.sAm != 1 || d.sAk == 1))) return XT_ERR_ARG;
   if (!akc && d.sAm != 1) return XT_ERR_ARG;
   if (!bkc && d.sBn != 1) return XT_ERR_ARG;
   // the kernel addresses a tile with 32-bit byte offsets from its origin
   const long lim = 1L << 32;
   if ((akc ? (256L * d.sAm + 32) : (32L * d.sAk + 256L)) * 8 >= lim) return XT_ERR_ARG;
+  // two-level rows: the whole row range sits in one 2 GB buffer window off the batch origin
+  if (d.rdiv > 0 && (((long)(d.M / d.rdiv) * d.sAm_hi + d.rdiv + 32L * d.sAk) * 8 >= (1L << 31))) return XT_ERR_ARG;
   if ((bkc ? (256L * d.sBn + 32) : (32L * d.sBk + 256L)) * 8 >= lim) return XT_ERR_ARG;
   GemmParams p; int cfg;
   plan_gemm(d, &p, &cfg);

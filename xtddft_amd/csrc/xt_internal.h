@@ -60,6 +60,11 @@ struct GemmDesc {
   double* C = nullptr;
   long ldc = 0, sCb1 = 0, sCb2 = 0;
   double alpha = 1.0, beta = 0.0;
+  // two-level rows (rdiv > 0; plain mode, A m-contiguous): row m = (hi, lo) = (m / rdiv,
+  // m % rdiv) sits at hi sAm_hi + lo in A and at hi sC_hi + lo ldc in C -- e.g. the stored
+  // exchange build's rows (i, j) over a padded MO factor and a padded Kx
+  int rdiv = 0;
+  long sAm_hi = 0, sC_hi = 0;
   int max_split = 0;                  // 0 = heuristic
   int tag = 0;                        // kernel identity for profiling (see xt_gemm.hip)
   double flops = 0.0;                 // algorithmic flops for profiling (0: 2 M N K R batch)
@@ -76,6 +81,7 @@ struct GemmParams {
   double alpha, beta;
   double* ws;
   XcFuse fz;
+  int rdiv; long sAm_hi, sC_hi;       // two-level rows (GemmDesc)
 };
 
 void plan_gemm(const GemmDesc& d, GemmParams* p, int* cfg);
