@@ -175,3 +175,25 @@ def test_range_separated_device_scf_equals_host(torch, kind):
     dev.kernel()
     assert dev.converged and dev.device_engine.B_lr is not None
     assert abs(dev.e_tot - host.e_tot) < 1e-9
+
+
+@pytest.mark.parametrize("kind", ["ROKS", "UKS"])
+def test_range_separated_spin_flip_matches_oracle(torch, kind):
+    """Spin-flip-up TDA (SF_TDA.py:408-585, ALDA0 kernel, K = hyb K + (alpha - hyb) K_LR
+    in the exchange block) and XSF-TDA (XSF_TDA.py:1455-1554; ROKS: SA = 3, remove; UKS:
+    USF, SA = 0) on the CAM-B3LYP mean field: device roots equal the oracle's explicit-A
+    eigenvalues.  Parity unpinned against the reference (no range-separated printout)."""
+    from oracle import xsf_tda as oxsf
+    from xtddft_amd import SF_TDA, XSF_TDA
+    mf = hf_meanfield(f"{kind}_CAMB3LYP")
+    vind, hdiag = osf.gen_tda_operation_sf(mf, 1)
+    w = np.linalg.eigvalsh(vind(np.eye(hdiag.size)).T)[:5]
+    e_ev, _ = SF_TDA(mf, isf=1).kernel(nstates=5)
+    assert np.abs(np.asarray(e_ev) / HA2EV - w).max() < 1e-7
+    o = oxsf.XSFOracle(mf)
+    vind, hdiag = o.gen_tda_operation_sf(fglobal=oxsf.default_fglobal(mf))
+    w = np.linalg.eigvalsh(vind(np.eye(hdiag.size)).T)[:5] * HA2EV_XSF
+    x = XSF_TDA(mf)
+    e_ev, _ = x.kernel(nstates=5)
+    assert np.all(x.converged)
+    assert np.abs(np.asarray(e_ev) - w).max() / HA2EV_XSF < 1e-7
