@@ -260,10 +260,10 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
       mma(p, b[p & 1]);
       __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);   // the first fragments
 #pragma unroll
-      for (int k = 0; k < NMF; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one DS read
-        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // up to two VALU
+      for (int k = 0; k < NMF / 2; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // two MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // two DS reads
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // up to four VALU
       }
       __builtin_amdgcn_sched_barrier(0);
     }
