@@ -260,10 +260,10 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
       mma(p, b[p & 1]);
       __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);   // the first fragments
 #pragma unroll
-      for (int k = 0; k < NMF / 2; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // two MFMAs
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // two DS reads
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // up to four VALU
+      for (int k = 0; k < NMF / 4; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // four MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);   // four DS reads
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);   // up to eight VALU
       }
       __builtin_amdgcn_sched_barrier(0);
     }
