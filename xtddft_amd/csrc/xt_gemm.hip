@@ -670,6 +670,7 @@ static const Cfg kCfg[] = {   // (bm, bn, bk, concurrent block slots, wgm, wgn)
   {256, 128, 16, 256, 4, 2},   // 6: 256x128, 8 waves of 64x64, BK 16 (tuning only)
   {128, 64, 16, 512, 2, 4},    // 7: 128x64, 8 waves of 64x16, BK 16, two blocks per CU
   {128, 128, 16, 512, 4, 2},   // 8: cfg 5 as 8 waves of 32x64 with rows on the SIMDs (ROWSIMD)
+  {128, 128, 32, 256, 4, 2},   // 9: cfg 8 with BK 32, one block per CU (both operands k-strided)
 };
 
 template <int BM, int BN, int WGM, int WGN, int BKT, int MINW, bool AK, bool BKc, int TAG, int MODE = 0,
@@ -831,6 +832,11 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
     };
     if (total(kCfg[8]) < 0.97 * total(kCfg[5])) cfg = 8;   // (model gains under 3 % measured neutral or worse)
   }
+  // both operands k-strided (rows of A and columns of B contiguous, e.g. XC back L): BK 32 with
+  // one block per CU halves the barriers per k and stages whole 256-B rows per k; rows on the
+  // SIMDs (back L 150.5 -> 143.7 ms same-box; BK 32 without ROWSIMD 145.2, and BK 32 for the
+  // k-contiguous forward U 132.9 -> 140.0, so it stays on this layout)
+  if (ff && d.M >= 96 && d.N >= 96) cfg = 9;
   const Cfg& c = kCfg[cfg];
   const long units = (long)p.R * ((d.K + c.bk - 1) / c.bk);
   int nsplit = choose_split(c, d.M, d.N, p.nbatch, units);
@@ -886,6 +892,7 @@ int dgemm(const GemmDesc& d, hipStream_t st, double* ws, size_t ws_bytes) {
     case 3: launch_cfg<64, 128, 2, 2, 32, 1>(p, st, akc, bkc, d.tag); break;
     case 5: launch_cfg<128, 128, 2, 4, 16, 4>(p, st, akc, bkc, d.tag); break;
     case 8: launch_cfg<128, 128, 4, 2, 16, 4, true>(p, st, akc, bkc, d.tag); break;
+    case 9: launch_cfg<128, 128, 4, 2, 32, 2, true>(p, st, akc, bkc, d.tag); break;
     default: launch_cfg<64, 64, 2, 2, 32, 2>(p, st, akc, bkc, d.tag); break;
   }
   if (p.nsplit > 1) {
