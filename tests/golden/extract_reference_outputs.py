@@ -15,6 +15,13 @@ Sources (PySCF 2.12.1 / libxc 7.0.0 runs recorded by the reference authors):
   UKS mf: SA=0, no OO compression) 10 roots in eV and the Delta<S^2> list.
 * ``example/spin up.ipynb`` cell 1 -- H 0 0 0; F 0 0 1.0 A ROKS/BHandHLYP aufbau
   triplet SCF energy.
+* ``example/TDA.ipynb`` (PySCF 2.11.0 / libxc 7.0.0), B3LYP / cc-pVDZ,
+  conv_tol 1e-11: cell 2 -- N2 RKS (shell / primitive / AO counts, nuclear
+  repulsion, total grid count, SCF energy, closed-shell TDA singlet roots);
+  cell 4 -- CH2O+ (``atom.ch2o_vacuum``) UKS: SCF energy and the U-TDA table
+  (energy eV, oscillator strength, Delta<S^2>, 12 roots); cell 6 -- the same
+  cation with ROKS: SCF energy and the X-TDA table (``XTDA.kernel``, the
+  headline operator kind).
 
 Only numbers are extracted (the fixture is data); no reference code is copied.
 """
@@ -83,6 +90,30 @@ def main():
     nb2 = json.load(open(os.path.join(REF, "spin up.ipynb")))
     up = "\n".join(_outputs(nb2["cells"][1]))
     out["roks_aufbau_hf_e_tot"] = float(re.search(r"converged SCF energy = ([-\d.]+)", up).group(1))
+
+    nb3 = json.load(open(os.path.join(REF, "TDA.ipynb")))
+    for cell, tag, head in ((2, "n2_rks_b3lyp", "TDA result is"),
+                            (4, "ch2o_uks_b3lyp", "UTDA result is"),
+                            (6, "ch2o_roks_b3lyp", "my XTDA result is")):
+        log = "\n".join(_outputs(nb3["cells"][cell]))
+        out[f"{tag}_counts"] = [int(re.search(rf"{k} = (\d+)", log).group(1))
+                                for k in ("number of shells", "number of NR pGTOs",
+                                          "number of NR cGTOs")]
+        out[f"{tag}_nuclear_repulsion"] = float(re.search(r"nuclear repulsion = ([-\d.]+)", log).group(1))
+        out[f"{tag}_tot_grids"] = int(re.search(r"tot grids = (\d+)", log).group(1))
+        out[f"{tag}_e_tot"] = float(re.search(r"converged SCF energy = ([-\d.]+)", log).group(1))
+        rows = []
+        for line in log[log.index(head):].splitlines()[2:]:
+            f = line.split()
+            if len(f) < 5 or not f[0].isdigit():
+                break
+            rows.append([float(x) for x in f[1:]])
+        rows = np.array(rows)
+        out[f"{tag}_td_ev"] = rows[:, 0].tolist()
+        out[f"{tag}_td_osc"] = rows[:, 2].tolist()
+        if rows.shape[1] > 4:
+            out[f"{tag}_td_delta_s2"] = rows[:, 4].tolist()
+    assert len(out["ch2o_roks_b3lyp_td_ev"]) == 12 and len(out["ch2o_uks_b3lyp_td_ev"]) == 12
 
     assert len(out["xsf_roks_alda0_ev"]) == 10 and len(out["usf_uks_alda0_ev"]) == 10
     assert len(out["hf_631g_grid_ang_F"]) == 75 and len(out["hf_631g_grid_ang_H"]) == 50

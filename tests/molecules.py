@@ -102,6 +102,40 @@ def fd_xc_response(scf, mfield, z, eps=1e-5):
     return out
 
 
+# example/TDA.ipynb (B3LYP / cc-pVDZ, conv_tol 1e-11): xtddft/utils/atom.py
+# ch2o_vacuum (CH2O+, charge 1, spin 1) and the N2 geometry the notebook printed
+CH2O_GEOM = ("C 0.000000 0.526270 0.000000; H 0.979180 1.091955 0.000000; "
+             "H -0.979175 1.091979 0.000000; O 0.000000 -0.667694 0.000000")
+N2_GEOM = "N 0 0 -0.55899578; N 0 0 0.55899578"
+
+
+@lru_cache(maxsize=None)
+def ch2o_mol():
+    return M(CH2O_GEOM, basis="cc-pvdz", charge=1, spin=1)
+
+
+@lru_cache(maxsize=None)
+def n2_mol():
+    return M(N2_GEOM, basis="cc-pvdz")
+
+
+@lru_cache(maxsize=None)
+def tda_scf(name: str):
+    """'CH2O_ROKS' / 'CH2O_UKS' / 'N2_UKS' (closed shell; = the notebook's RKS):
+    B3LYP / cc-pVDZ, converged like the notebook (conv_tol 1e-11)."""
+    mol = ch2o_mol() if name.startswith("CH2O") else n2_mol()
+    mf = (ROKS if name.endswith("ROKS") else UKS)(mol, "b3lyp")
+    mf.conv_tol = 1e-11
+    mf.kernel()
+    assert mf.converged
+    return mf
+
+
+@lru_cache(maxsize=None)
+def tda_meanfield(name: str):
+    return tda_scf(name).to_meanfield()
+
+
 HF_POL_BASIS = None
 
 

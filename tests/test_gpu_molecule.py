@@ -84,6 +84,32 @@ def test_xtda_on_roks_molecule_matches_oracle(torch):
         assert abs(f[sel].sum() - f_ref[sel].sum()) <= 1e-5 * max(f_ref[sel].sum(), 1e-6)
 
 
+@pytest.mark.parametrize("jk_mode", ["DF", "ERI8"])
+@pytest.mark.parametrize("name,tag", [("CH2O_ROKS", "ch2o_roks_b3lyp"), ("CH2O_UKS", "ch2o_uks_b3lyp")])
+def test_xtda_kernel_matches_reference_printout(torch, name, tag, jk_mode):
+    """XTDA(mol, mf).kernel() with nstates = 12 on CH2O+ / B3LYP / cc-pVDZ
+    (example/TDA.ipynb cells 6 (ROKS: X-TDA) and 4 (UKS: U-TDA)): device operator
+    + device Davidson against the printed table -- excitation energies, oscillator
+    strengths and (X-TDA) Delta<S^2>, all printed with 4 decimals (|ours - printed| <= 5e-5
+    from the rounding, plus the solver's residual tolerance 1e-5).  jk_mode DF is the
+    exact Cholesky factor of the ERIs, ERI8 the stored 8-fold ERIs the device
+    factorises itself: both are the reference's exact (non-DF) J/K."""
+    from molecules import tda_meanfield
+    from xtddft_amd import XTDA
+    mf = tda_meanfield(name)
+    if jk_mode == "ERI8":
+        mf = as_device_eri8(mf)
+    x = XTDA(mf.mol, mf, nstates=12)
+    e = x.kernel()
+    assert np.all(x.converged)
+    ref = reference_outputs()
+    tol = 6e-5
+    assert np.abs(np.asarray(e) * HA2EV - ref[f"{tag}_td_ev"]).max() < tol
+    if name.endswith("ROKS"):   # cell 4's Delta<S^2> is UTDA.py's UKS formula, not XTDA.py:831-836
+        assert np.abs(x.dS2 - ref[f"{tag}_td_delta_s2"]).max() < tol
+    assert np.abs(x.osc_str() - ref[f"{tag}_td_osc"]).max() < tol
+
+
 def test_sf_up_on_aufbau_triplet_matches_oracle(torch):
     """SF-TDA spin-flip-up (SF_TDA.py:408-585) on the spin-up notebook's ROKS triplet."""
     from xtddft_amd import SF_TDA
