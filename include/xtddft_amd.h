@@ -167,6 +167,15 @@ int xt_xsf_j_diagonals(xt_ctx* ctx, double* co_j, double* ov_j, int ptr_kind);
 int xt_dgemm(int transa, int transb, int m, int n, int k, double alpha,
              const double* a, long lda, const double* b, long ldb, double beta,
              double* c, long ldc, void* hip_stream);
+/* C[b] = alpha * sum_r A[b,r] B[b,r] + beta * C[b] with explicit strides: A(m, k) at
+   a + b sAb + r sAr + m sAm + k sAk (sAm or sAk = 1), B(k, n) likewise (sBk or sBn = 1),
+   C row-major with ldc, batch stride sCb.  The strided, reduce-indexed contraction the
+   MO transforms and J/K builds run (lib.einsum over the DF index behind get_jk,
+   XTDA.py:518-543); exposed so every engine layout is testable. */
+int xt_dgemm_strided(int m, int n, int k, int r, int nbatch, double alpha,
+                     const double* a, long sAm, long sAk, long sAr, long sAb,
+                     const double* b, long sBk, long sBn, long sBr, long sBb, double beta,
+                     double* c, long ldc, long sCb, void* hip_stream);
 /* y = (x - e*w) / clamp(d - (e - shift)) row-wise; diag preconditioner
    (XTDA.py:736-744, PySCF make_diag_precond). nrow vectors of length dim. */
 int xt_precond(int nrow, int dim, const double* diag, const double* e, double shift,

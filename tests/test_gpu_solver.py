@@ -39,6 +39,34 @@ def test_dgemm_layouts(torch, hiplib, m, n, k, ta, tb):
     assert float((c - ref).abs().max()) / scale < 1e-13 * max(1, k) ** 0.5
 
 
+@pytest.mark.parametrize("m,n,k,r,nb", [(200, 301, 77, 3, 1), (128, 96, 40, 2, 2), (97, 130, 33, 1, 1),
+                                         (300, 250, 1000, 4, 1)])
+@pytest.mark.parametrize("ak,bk", [(False, False), (True, False), (False, True), (True, True)])
+def test_dgemm_strided_reduce_index(torch, hiplib, m, n, k, r, nb, ak, bk):
+    """xt_dgemm_strided: C[b] = alpha sum_r A[b,r] B[b,r] + beta C[b] against torch for
+    every operand layout (ak: A k-contiguous, bk: B k-contiguous), a reduce index
+    r > 1 and ragged K (K % 32 != 0) -- (False, False) with M, N >= 96 is the BK-32
+    rows-on-SIMD tile and its masked ragged-K instantiation."""
+    from xtddft_amd import _capi
+    g = torch.Generator(device="cuda").manual_seed(m + 3 * n + 7 * k + r)
+    # A as (nb, r, m, k) k-contiguous or (nb, r, k, m) m-contiguous; B as (nb, r, k, n) or (nb, r, n, k)
+    a = torch.randn((nb, r, m, k) if ak else (nb, r, k, m), dtype=torch.float64, device="cuda", generator=g)
+    b = torch.randn((nb, r, n, k) if bk else (nb, r, k, n), dtype=torch.float64, device="cuda", generator=g)
+    c = torch.randn((nb, m, n), dtype=torch.float64, device="cuda", generator=g)
+    am = a if ak else a.transpose(2, 3)
+    bm = b.transpose(2, 3) if bk else b
+    ref = 0.7 * torch.einsum("brmk,brkn->bmn", am, bm) - 0.3 * c
+    sAm, sAk = (k, 1) if ak else (1, m)
+    sBk, sBn = (1, k) if bk else (n, 1)
+    st = torch.cuda.current_stream().cuda_stream
+    _capi.check(hiplib.xt_dgemm_strided(m, n, k, r, nb, 0.7, a.data_ptr(), sAm, sAk, m * k, r * m * k,
+                                        b.data_ptr(), sBk, sBn, k * n, r * k * n, -0.3, c.data_ptr(), n, m * n,
+                                        ctypes.c_void_p(st)), "dgemm_strided")
+    torch.cuda.synchronize()
+    scale = max(1.0, float(ref.abs().max()))
+    assert float((c - ref).abs().max()) / scale < 1e-13 * (r * k) ** 0.5
+
+
 def test_davidson_matches_oracle_davidson(torch):
     from xtddft_amd.davidson import DiagPrecond, davidson1
     from xtddft_amd.operator import DeviceOperator

@@ -28,7 +28,7 @@ EXPORTS = [
     "xt_set_jk_eri8", "xt_naux",
     "xt_set_grid", "xt_set_oo_basis", "xt_apply", "xt_dim", "xt_last_timings",
     "xt_xsf_j_diagonals", "xt_set_exchange_mode", "xt_prepare", "xt_set_partition", "xt_set_profile",
-    "xt_profile_stats", "xt_profile_bytes", "xt_dgemm", "xt_precond", "xt_row_norms2", "xt_row_scale", "xt_build_id",
+    "xt_profile_stats", "xt_profile_bytes", "xt_dgemm", "xt_dgemm_strided", "xt_precond", "xt_row_norms2", "xt_row_scale", "xt_build_id",
     "xt_int3c2e_cart", "xt_int2e_cart", "xt_eval_ao",
 ]
 
@@ -98,6 +98,8 @@ def lib():
     L.xt_profile_bytes.argtypes = [vp, c_int, dp]
     L.xt_dgemm.argtypes = [c_int, c_int, c_int, c_int, c_int, c_double, dp, c_long, dp, c_long,
                            c_double, dp, c_long, vp]
+    L.xt_dgemm_strided.argtypes = [c_int, c_int, c_int, c_int, c_int, c_double, dp, c_long, c_long, c_long, c_long,
+                                   dp, c_long, c_long, c_long, c_long, c_double, dp, c_long, c_long, vp]
     L.xt_precond.argtypes = [c_int, c_int, dp, dp, c_double, dp, dp, vp]
     L.xt_row_norms2.argtypes = [c_int, c_int, dp, dp, vp]
     L.xt_row_scale.argtypes = [c_int, c_int, dp, dp, vp]

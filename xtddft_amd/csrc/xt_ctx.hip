@@ -1386,6 +1386,8 @@ extern "C" int xt_xsf_j_diagonals(xt_ctx* c, double* co_j, double* ov_j, int ptr
 // ---------------------------------------------------------------------------
 // device linear algebra for the Davidson solver
 // ---------------------------------------------------------------------------
+static int run_desc(const GemmDesc& g, void* stream);
+
 extern "C" int xt_dgemm(int transa, int transb, int m, int n, int k, double alpha,
                         const double* a, long lda, const double* b, long ldb, double beta,
                         double* cc, long ldc, void* stream) {
@@ -1394,6 +1396,25 @@ extern "C" int xt_dgemm(int transa, int transb, int m, int n, int k, double alph
   g.A = a; if (transa) { g.sAm = 1; g.sAk = lda; } else { g.sAm = lda; g.sAk = 1; }
   g.B = b; if (transb) { g.sBk = 1; g.sBn = ldb; } else { g.sBk = ldb; g.sBn = 1; }
   g.C = cc; g.ldc = ldc; g.alpha = alpha; g.beta = beta;
+  return run_desc(g, stream);
+}
+
+extern "C" int xt_dgemm_strided(int m, int n, int k, int r, int nbatch, double alpha,
+                                const double* a, long sAm, long sAk, long sAr, long sAb,
+                                const double* b, long sBk, long sBn, long sBr, long sBb, double beta,
+                                double* cc, long ldc, long sCb, void* stream) {
+  if (m < 0 || n < 0 || k < 0 || r < 1 || nbatch < 1) return fail(XT_ERR_ARG, "xt_dgemm_strided: bad sizes");
+  if (sAm != 1 && sAk != 1) return fail(XT_ERR_ARG, "xt_dgemm_strided: A needs a unit m or k stride");
+  if (sBn != 1 && sBk != 1) return fail(XT_ERR_ARG, "xt_dgemm_strided: B needs a unit k or n stride");
+  GemmDesc g;
+  g.M = m; g.N = n; g.K = k; g.R = r; g.nb1 = nbatch;
+  g.A = a; g.sAm = sAm; g.sAk = sAk; g.sAr = sAr; g.sAb1 = sAb;
+  g.B = b; g.sBk = sBk; g.sBn = sBn; g.sBr = sBr; g.sBb1 = sBb;
+  g.C = cc; g.ldc = ldc; g.sCb1 = sCb; g.alpha = alpha; g.beta = beta;
+  return run_desc(g, stream);
+}
+
+static int run_desc(const GemmDesc& g, void* stream) {
   // split-K workspace per HIP device (the caller's current device owns the
   // stream and the operands)
   int dev = 0;

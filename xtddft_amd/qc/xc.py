@@ -67,6 +67,10 @@ import math
 import numpy as np
 
 DENS_THRESHOLD = 1e-14
+_ZETA_MAX = 1.0 - 1e-10          # |zeta| cap (libxc's zeta threshold): (1 -+ zeta)^(-4/3) stays finite
+# spin-separable exchange pieces: each spin channel's half is screened on its own
+# density, as libxc does for exchange; correlation sees both channels unscreened
+_EXCHANGE = ("slater", "b88", "tpss_x")
 
 _CX = 1.5 * (3.0 / (4.0 * math.pi)) ** (1.0 / 3.0)
 
@@ -181,7 +185,7 @@ def _vwn_fit(prm, i, x, torch):
 def _vwn_parts(ra, rb, torch):
     rho = ra + rb
     x = (3.0 / (4.0 * math.pi * rho)) ** (1.0 / 6.0)
-    z = (ra - rb) / rho
+    z = torch.clamp((ra - rb) / rho, -_ZETA_MAX, _ZETA_MAX)     # libxc's zeta threshold
     fz = ((1.0 + z) ** (4.0 / 3.0) + (1.0 - z) ** (4.0 / 3.0) - 2.0) / (2.0 ** (4.0 / 3.0) - 2.0)
     return rho, x, z, fz
 
@@ -201,7 +205,6 @@ def _vwn_rpa(ra, rb, saa, sab, sbb, torch):
 
 
 # ---------------------------------------------------------------- TPSS (meta-GGA)
-_ZETA_MAX = 1.0 - 1e-10          # |zeta| cap (libxc's zeta threshold): (1 -+ zeta)^(-4/3) stays finite
 _TAU_MIN = 1e-30
 
 
@@ -329,15 +332,29 @@ _PIECES = {"slater": _slater, "b88": _b88, "lyp": _lyp, "vwn5": _vwn5, "vwn_rpa"
 _MPIECES = {"tpss_x": _tpss_x, "tpss_c": _tpss_c}
 
 
-def _energy_density(comps, ra, rb, saa, sab, sbb, ta, tb, torch):
+def _piece(name, ra, rb, saa, sab, sbb, ta, tb, torch):
+    if name.startswith("ityh_b88@"):
+        return _ityh_b88(ra, rb, saa, sab, sbb, torch, float(name.split("@")[1]))
+    if name in _MPIECES:
+        return _MPIECES[name](ra, rb, saa, sab, sbb, ta, tb, torch)
+    return _PIECES[name](ra, rb, saa, sab, sbb, torch)
+
+
+def _energy_density(comps, ra, rb, saa, sab, sbb, ta, tb, torch, on=None):
+    """Sum of the functional's pieces.  ``on`` = (on_a, on_b): 0/1 constants marking
+    where each channel's density exceeds DENS_THRESHOLD; an exchange piece's half of a
+    channel below it is dropped (with the other channel's arguments replaced by inert
+    constants, so no derivative reaches the vanishing channel)."""
     eps = 0.0
     for name, coef in comps:
-        if name.startswith("ityh_b88@"):
-            eps = eps + coef * _ityh_b88(ra, rb, saa, sab, sbb, torch, float(name.split("@")[1]))
-        elif name in _MPIECES:
-            eps = eps + coef * _MPIECES[name](ra, rb, saa, sab, sbb, ta, tb, torch)
+        if on is not None and (name in _EXCHANGE or name.startswith("ityh_b88@")):
+            tiny = torch.full_like(ra, 1e-30).detach()
+            zero = torch.zeros_like(ra).detach()
+            half_a = _piece(name, ra, tiny, saa, zero, zero, ta, None if tb is None else tiny, torch)
+            half_b = _piece(name, tiny, rb, zero, zero, sbb, None if ta is None else tiny, tb, torch)
+            eps = eps + coef * (on[0] * half_a + on[1] * half_b)
         else:
-            eps = eps + coef * _PIECES[name](ra, rb, saa, sab, sbb, torch)
+            eps = eps + coef * _piece(name, ra, rb, saa, sab, sbb, ta, tb, torch)
     return eps
 
 
@@ -387,7 +404,9 @@ def _eval_xc_eff(torch, xc, rho, deriv):
     else:
         saa = sab = sbb = torch.zeros_like(ra)
     ta, tb = (rs[0, 4], rs[1, 4]) if ncomp == 5 else (None, None)
-    eps = _energy_density(comps, ra, rb, saa, sab, sbb, ta, tb, torch)
+    on = ((rs[0, 0] > DENS_THRESHOLD).to(torch.float64).detach(),
+          (rs[1, 0] > DENS_THRESHOLD).to(torch.float64).detach())
+    eps = _energy_density(comps, ra, rb, saa, sab, sbb, ta, tb, torch, on)
     g = torch.autograd.grad(eps.sum(), x, create_graph=deriv >= 2)[0]
     exc[mask] = (eps / (ra + rb)).detach().numpy()
     vxc[:, :, mask] = g.detach().numpy().reshape(2, ncomp, -1)
@@ -398,14 +417,16 @@ def _eval_xc_eff(torch, xc, rho, deriv):
             H[k] = torch.autograd.grad(g[k].sum(), x, retain_graph=k < n - 1)[0].numpy()
         H = 0.5 * (H + H.transpose(1, 0, 2))       # exact symmetry (autograd round-off)
         fxc[..., mask] = H.reshape(2, ncomp, 2, ncomp, -1)
-    _screen_spin(rho, vxc, fxc, np)
+    if xctype == "MGGA":
+        _screen_spin(rho, vxc, fxc, np)
     return exc, vxc, fxc
 
 
 def _screen_spin(rho, vxc, fxc, xp):
-    """A spin channel without density at a point (below DENS_THRESHOLD) carries no
-    potential or kernel there (libxc's per-spin screening; TPSS correlation's
-    fully polarised terms are singular in a vanishing channel)."""
+    """Meta-GGA only: a spin channel without density at a point (below DENS_THRESHOLD)
+    carries no potential or kernel there (TPSS correlation's fully polarised terms are
+    singular in a vanishing channel).  LDA / GGA functionals screen only their
+    exchange halves per channel (``_energy_density``), as libxc does."""
     for s in range(2):
         off = rho[s, 0] < DENS_THRESHOLD
         if not bool(off.any()):
@@ -448,7 +469,9 @@ def eval_xc_eff_torch(xc: str, rho, deriv: int = 1):
     else:
         saa = sab = sbb = torch.zeros_like(ra)
     ta, tb = (rs[0, 4], rs[1, 4]) if ncomp == 5 else (None, None)
-    eps = _energy_density(comps, ra, rb, saa, sab, sbb, ta, tb, torch)
+    on = ((rs[0, 0] > DENS_THRESHOLD).to(torch.float64).detach(),
+          (rs[1, 0] > DENS_THRESHOLD).to(torch.float64).detach())
+    eps = _energy_density(comps, ra, rb, saa, sab, sbb, ta, tb, torch, on)
     g = torch.autograd.grad(eps.sum(), x, create_graph=deriv >= 2)[0]
     exc[idx] = (eps / (ra + rb)).detach()
     vxc[:, :, idx] = g.detach().reshape(2, ncomp, -1)
@@ -459,5 +482,6 @@ def eval_xc_eff_torch(xc: str, rho, deriv: int = 1):
             H[k] = torch.autograd.grad(g[k].sum(), x, retain_graph=k < n - 1)[0]
         H = 0.5 * (H + H.transpose(0, 1))
         fxc[..., idx] = H.reshape(2, ncomp, 2, ncomp, -1)
-    _screen_spin(rho, vxc, fxc, torch)
+    if xctype == "MGGA":
+        _screen_spin(rho, vxc, fxc, torch)
     return exc, vxc, fxc
