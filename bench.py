@@ -650,7 +650,8 @@ def rank_main(args):
         roofline=roofline,
         gemm_classes=others,
         phases_ms_last_step=phases,
-        setup_s=dict(synthetic_generation=round(w.t_gen, 2), operator_construction=round(w.t_op, 2)),
+        setup_s=dict(synthetic_generation=round(w.t_gen, 2), operator_construction=round(w.t_op, 2),
+                     construction_phases={k: round(v, 3) for k, v in getattr(op, "setup_s", {}).items()}),
         exchange=dict(mode=op.k_mode, stored_gib=round(op.k_gib, 2), build_s=round(op.prepare_s, 3)),
     )
     if verify is not None:

@@ -110,6 +110,21 @@ def test_xtda_kernel_matches_reference_printout(torch, name, tag, jk_mode):
     assert np.abs(x.osc_str() - ref[f"{tag}_td_osc"]).max() < tol
 
 
+def test_utda_closed_shell_n2_contains_reference_tda_singlets(torch):
+    """N2 / B3LYP / cc-pVDZ (example/TDA.ipynb cell 2): U-TDA on the closed-shell UKS
+    mean field through the device operator (explicit A from device columns, host
+    eigh: XTDA.full_diag) spans singlets and triplets; every printed TDA singlet root
+    (4 decimals, eV) is one of its eigenvalues."""
+    from molecules import tda_meanfield
+    from xtddft_amd import XTDA
+    mf = tda_meanfield("N2_UKS")
+    x = XTDA(mf.mol, mf, nstates=60, use_Davidson=False)
+    x.kernel()
+    w = np.linalg.eigvalsh(x.A) * HA2EV
+    for e in reference_outputs()["n2_rks_b3lyp_td_ev"]:
+        assert np.abs(w - e).min() < 6e-5, e
+
+
 def test_sf_up_on_aufbau_triplet_matches_oracle(torch):
     """SF-TDA spin-flip-up (SF_TDA.py:408-585) on the spin-up notebook's ROKS triplet."""
     from xtddft_amd import SF_TDA

@@ -190,43 +190,40 @@ k_xc_rho_w(int O, int nx, int V, int n,
     for (int j = 0; j < TNG; ++j) dst[j] = src[(16 * j * PP) / 2];
   };
   // one k-step from ring slot SL and B buffer BB, half SUB of the pair; ZERO: the first
-  // k-step of the a-tile, into a zero accumulator; NT_: the a-tile's live row sub-tiles
-  // (1 for a last a-tile with V % 32 <= 16: its second sub-tile is all padding)
-  auto step = [&](auto SL, auto BB, auto SUB, auto ZERO, auto NT_) XT_INLINE {
+  // k-step of the a-tile, into a zero accumulator
+  auto step = [&](auto SL, auto BB, auto SUB, auto ZERO) XT_INLINE {
     constexpr int sl = decltype(SL)::value, bb = decltype(BB)::value, sub = decltype(SUB)::value;
-    load_z((sl + ZD - 1) % ZD);   // into the slot the previous k-step consumed (whole ring rows)
+    load_z((sl + ZD - 1) % ZD);   // into the slot the previous k-step consumed
 #pragma unroll
-    for (int t = 0; t < decltype(NT_)::value; ++t)
+    for (int t = 0; t < TMA; ++t)
 #pragma unroll
       for (int j = 0; j < TNG; ++j)
         acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(
             zq[sl][t], bq[bb][j][sub], decltype(ZERO)::value ? (d4w){0.0, 0.0, 0.0, 0.0} : acc[t][j], 0, 0, 0);
   };
   // one k-step pair in ring slots SL, SL + 1 from B buffer BB; prefetches pair pn's B
-  auto kpair = [&](auto SL, auto BB, auto ZERO, auto NT_, int pn) XT_INLINE {
+  auto kpair = [&](auto SL, auto BB, auto ZERO, int pn) XT_INLINE {
     constexpr int sl = decltype(SL)::value, bb = decltype(BB)::value;
     bread(pn, bq[bb ^ 1]);
-    step(std::integral_constant<int, sl>{}, BB, std::integral_constant<int, 0>{}, ZERO, NT_);
+    step(std::integral_constant<int, sl>{}, BB, std::integral_constant<int, 0>{}, ZERO);
     step(std::integral_constant<int, (sl + 1) % ZD>{}, BB, std::integral_constant<int, 1>{},
-         std::integral_constant<bool, false>{}, NT_);
+         std::integral_constant<bool, false>{});
   };
   using F = std::integral_constant<bool, false>;
   using T1 = std::integral_constant<bool, true>;
 
-  // one a-tile: ring phase P (slot of its first k-step), weight buffer BUF and live row
-  // sub-tiles NT_ compile-time
-  auto tile = [&](auto PH, auto BUF, auto NT_, int at) XT_INLINE {
-    constexpr int P = decltype(PH)::value, B = decltype(BUF)::value, NTL = decltype(NT_)::value;
+  // one a-tile: ring phase P (slot of its first k-step) and weight buffer BUF compile-time
+  auto tile = [&](auto PH, auto BUF, int at) XT_INLINE {
+    constexpr int P = decltype(PH)::value, B = decltype(BUF)::value;
     if (at + 1 < nat) load_w(at + 1);
     if (wave_on) {
-      kpair(std::integral_constant<int, P>{}, std::integral_constant<int, 0>{}, T1{}, NT_, p_lo + 1);
+      kpair(std::integral_constant<int, P>{}, std::integral_constant<int, 0>{}, T1{}, p_lo + 1);
       int k = 1;
       for (; k + 2 <= np; k += 2) {
-        kpair(std::integral_constant<int, (P + 2) % ZD>{}, std::integral_constant<int, 1>{}, F{}, NT_, p_lo + k + 1);
-        kpair(std::integral_constant<int, P>{}, std::integral_constant<int, 0>{}, F{}, NT_, p_lo + k + 2);
+        kpair(std::integral_constant<int, (P + 2) % ZD>{}, std::integral_constant<int, 1>{}, F{}, p_lo + k + 1);
+        kpair(std::integral_constant<int, P>{}, std::integral_constant<int, 0>{}, F{}, p_lo + k + 2);
       }
-      if (k < np)
-        kpair(std::integral_constant<int, (P + 2) % ZD>{}, std::integral_constant<int, 1>{}, F{}, NT_, p_lo + k + 1);
+      if (k < np) kpair(std::integral_constant<int, (P + 2) % ZD>{}, std::integral_constant<int, 1>{}, F{}, p_lo + k + 1);
       bread(p_lo, bq[0]);        // the next a-tile's first pair (the PhiO image never changes)
       // contraction with the a-tile's weights: acc[t][j][r] = T[a = 16 t + q + 4 r][g = 16 j + r16].
       // Half a row (t, r) of weights at a time, the next half's reads issued before this
@@ -244,8 +241,8 @@ k_xc_rho_w(int O, int nx, int V, int n,
       };
       wread(0, wb[0]);
 #pragma unroll
-      for (int hh = 0; hh < 8 * NTL; ++hh) {
-        if (hh + 1 < 8 * NTL) wread(hh + 1, wb[(hh + 1) & 1]);
+      for (int hh = 0; hh < 8 * TMA; ++hh) {
+        if (hh + 1 < 8 * TMA) wread(hh + 1, wb[(hh + 1) & 1]);
         const int rw_ = hh / 2, j0 = (hh % 2) * JH;
         const int t = rw_ / 4, r = rw_ % 4;
 #pragma unroll
@@ -267,28 +264,15 @@ k_xc_rho_w(int O, int nx, int V, int n,
     for (int d = 0; d < ZD - 1; ++d) load_z(d);
     bread(p_lo, bq[0]);
   }
-  // a-tiles in pairs: with an odd pair count per a-tile the ring phase alternates 0, 2.
-  // A last a-tile holding <= 16 live virtuals (V = 901: 5) runs one row sub-tile.
-  using NF = std::integral_constant<int, TMA>;
-  using NH = std::integral_constant<int, 1>;
-  const bool half_last = (V % WA) != 0 && (V % WA) <= 16;
-  const int nfull = half_last ? nat - 1 : nat;
+  // a-tiles in pairs: with an odd pair count per a-tile the ring phase alternates 0, 2
   auto run = [&](auto ALT) XT_INLINE {
     constexpr int P1 = decltype(ALT)::value ? 2 : 0;
-    using Q0 = std::integral_constant<int, 0>;
-    using Q1 = std::integral_constant<int, P1>;
-    using B0 = std::integral_constant<int, 0>;
-    using B1 = std::integral_constant<int, 1>;
     int at = 0;
-    for (; at + 2 <= nfull; at += 2) {
-      tile(Q0{}, B0{}, NF{}, at);
-      tile(Q1{}, B1{}, NF{}, at + 1);
+    for (; at + 2 <= nat; at += 2) {
+      tile(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, at);
+      tile(std::integral_constant<int, P1>{}, std::integral_constant<int, 1>{}, at + 1);
     }
-    if (at < nfull) tile(Q0{}, B0{}, NF{}, at++);
-    if (half_last) {     // a-tile `at`: phase and buffer by its parity
-      if (at & 1) tile(Q1{}, B1{}, NH{}, at);
-      else tile(Q0{}, B0{}, NH{}, at);
-    }
+    if (at < nat) tile(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, at);
   };
   if (np & 1) run(T1{});
   else run(F{});

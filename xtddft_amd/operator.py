@@ -123,12 +123,14 @@ class DeviceOperator:
         self.stream = stream
         _capi.check(L.xt_set_stream(h, ctypes.c_void_p(stream or 0)), "xt_set_stream")
         self.dim = L.xt_dim(h)
+        self.setup_s = {}
         self._setup()
         if self.replicate_df:
             self._set_partition(kind, nc, no)
         _capi.check(L.xt_set_exchange_mode(h, _capi.K_MODE[k_mode], float(k_max_gib)),
                     "xt_set_exchange_mode")
         self.prepare()
+        self.setup_s["prepare"] = self.prepare_s
 
     def _set_partition(self, kind, nc, no):
         """Aux window and exchange row block of this rank (xt_set_partition)."""
@@ -152,8 +154,23 @@ class DeviceOperator:
         return self.k_mode
 
     # -------------------------------------------------------------- setup
+    def _sync(self):
+        t = _torch()
+        if t is not None and t.cuda.is_available():
+            t.cuda.synchronize(self.desc.device)
+
+    def _lap(self, name, t0):
+        """Setup phase timer (the phases enqueue device work: synchronised at each lap)."""
+        import time
+        self._sync()
+        t1 = time.perf_counter()
+        self.setup_s[name] = self.setup_s.get(name, 0.0) + (t1 - t0)
+        return t1
+
     def _setup(self):
+        import time
         L, h, mf = self._L, self._h, self.mf
+        t = time.perf_counter()
         if mf.is_rohf:
             ca = mf.mo_coeff; cb = None
         else:
@@ -161,6 +178,7 @@ class DeviceOperator:
         pa, ka, ra = _ptr(ca)
         pb, _, rb = _ptr(cb)
         _capi.check(L.xt_set_orbitals(h, pa, pb, ka), "xt_set_orbitals")
+        t = self._lap("orbitals", t)
         fa, fb = mf.fock_mo()
         fah, fbh = mf.fock_mo_hf()
         ptrs = [_ptr(x) for x in (fa, fb, fah, fbh)]
@@ -169,6 +187,7 @@ class DeviceOperator:
             e = [_ptr(mf.mo_energy[0]), _ptr(mf.mo_energy[1])]
             _capi.check(L.xt_set_orbital_energies(h, e[0][0], e[1][0], _capi.XT_PTR_HOST),
                         "xt_set_orbital_energies")
+        t = self._lap("fock_mo", t)
         p0, p1 = self.aux_range
         if mf.jk_mode == "ERI8":
             # stored ERIs: factorised on the device; this rank keeps its block
@@ -187,6 +206,7 @@ class DeviceOperator:
             if mf.cderi_lr is not None and mf.omega != 0:
                 pl, kl, rl = _ptr(mf.cderi_lr[p0:p1])
                 _capi.check(L.xt_set_jk_df(h, pl, 1, kl), "xt_set_jk_df(lr)")
+        t = self._lap("jk_factor", t)
         g0, g1 = self.grid_range
         if g1 > g0:
             grids = mf.grids
@@ -204,6 +224,7 @@ class DeviceOperator:
             if not (kao == kw == kk):
                 raise TypeError("grid arrays must all be host or all device")
             _capi.check(L.xt_set_grid(h, pao, pw, pk, kao), "xt_set_grid")
+        self._lap("grid", t)
 
     def naux(self):
         """(DF / Cholesky functions on this rank, full Cholesky rank of an ERI8 factorisation)."""
