@@ -796,6 +796,9 @@ static int resolve_kmode(xt_ctx* c) {
   return 0;
 }
 
+// occupied rows per stored-exchange build GEMM (the fold of the symmetric build, build_kx)
+constexpr int KX_FOLD = 8;
+
 static int build_kx(xt_ctx* c) {
   const int O = c->O, V = c->V, nmo = c->d.nmo, naux = c->d.naux;
   const long mm = (long)nmo * nmo;
@@ -817,18 +820,29 @@ static int build_kx(xt_ctx* c) {
       const double* Bo = bmo_full(c, B, gr[q].ob);   // all aux rows: Kx sums over every P
       const double* Bv = bmo_full(c, B, gr[q].vb) + (long)c->v0 * nmo + c->v0;
       // batch a: Kx[(i,a)][(j,b)] += coef sum_P Bo[P][i][j] Bv[P][a][b] with rows (i, j) of
-      // all this context's i in one GEMM (two-level rows: i strides nmo in Bo and V ld in
-      // Kx, j strides 1 and V) -- one launch of (i1 - i0) O rows instead of one per i,
-      // whose O = 101 rows filled 101 / 128 of a row tile
-      GemmDesc g;
-      g.M = (i1 - i0) * O; g.N = V; g.K = naux; g.nb1 = V;
-      g.rdiv = O; g.sAm_hi = nmo; g.sC_hi = (long)V * ld;
-      g.A = Bo + (long)i0 * nmo; g.sAm = 1; g.sAk = mm; g.sAb1 = 0;
-      g.B = Bv; g.sBk = mm; g.sBn = 1; g.sBb1 = nmo;
-      g.C = K + (size_t)i0 * V * ld; g.ldc = V; g.sCb1 = (long)ld;
-      g.alpha = coef; g.beta = 1.0;
-      RET(gemm(c, g));
+      // a chunk of KX_FOLD occupied i in one GEMM (two-level rows: i strides nmo in Bo and
+      // V ld in Kx, j strides 1 and V).  Kx is symmetric under (i,a) <-> (j,b), so a chunk
+      // [ci, ce) computes only j >= ci (and the j < i0 outside this context's rows); the
+      // blocks (i, j) with i0 <= j < ci are transposes of blocks built by earlier chunks
+      // and are mirrored afterwards: ~54 % of the full build's flops at O = 101.
+      for (int ci = i0; ci < i1; ci += KX_FOLD) {
+        const int ce = ci + KX_FOLD < i1 ? ci + KX_FOLD : i1;
+        const int jr[2][2] = {{0, i0}, {ci, O}};
+        for (int r = 0; r < 2; ++r) {
+          const int j0 = jr[r][0], j1 = jr[r][1];
+          if (j1 <= j0) continue;
+          GemmDesc g;
+          g.M = (ce - ci) * (j1 - j0); g.N = V; g.K = naux; g.nb1 = V;
+          g.rdiv = j1 - j0; g.sAm_hi = nmo; g.sC_hi = (long)V * ld;
+          g.A = Bo + (long)ci * nmo + j0; g.sAm = 1; g.sAk = mm; g.sAb1 = 0;
+          g.B = Bv; g.sBk = mm; g.sBn = 1; g.sBb1 = nmo;
+          g.C = K + (size_t)ci * V * ld + (size_t)j0 * V; g.ldc = V; g.sCb1 = (long)ld;
+          g.alpha = coef; g.beta = 1.0;
+          RET(gemm(c, g));
+        }
+      }
     }
+    kx_mirror(c->st, O, V, (long)ld, i0, i1, KX_FOLD, K);
   }
   HIPCHK(hipStreamSynchronize(c->st));
   c->kx_valid = true;

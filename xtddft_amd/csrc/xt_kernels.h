@@ -33,6 +33,9 @@ void xsf_combine4(hipStream_t st, int nz, int O, int V, int nc, int no, const W1
                   double* acc);
 void xsf_extract(hipStream_t st, int nz, int nc, int no, int nv, int remove, const double* vects, const double* full, double* out);
 void xsf_jdiag(hipStream_t st, int naux, int nmo, int nc, int no, int nv, const double* bmo, double* co_j, double* ov_j);
+// stored exchange: blocks (i, j), i0 <= j < i0 + fold floor((i - i0) / fold), of K (row (i,a) at
+// (i V + a) ld, column (j,b) at j V + b) set to the transposes of blocks (j, i)
+void kx_mirror(hipStream_t st, int O, int V, long ld, int i0, int i1, int fold, double* K);
 void precond(hipStream_t st, int nrow, int dim, const double* diag, const double* e, double shift, const double* r, double* out);
 void row_norms2(hipStream_t st, int nrow, int dim, const double* x, double* out);
 void row_scale(hipStream_t st, int nrow, int dim, double* x, const double* s);

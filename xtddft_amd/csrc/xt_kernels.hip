@@ -745,6 +745,39 @@ void extract_xtda(hipStream_t st, int nz, int nc, int no, int nv, const double* 
 void extract_one(hipStream_t st, int nz, int O, int V, const double* acc, const double* kx, double* out) {
   hipLaunchKernelGGL(k_extract_one, dim3(nblocks((long)nz * O * V)), dim3(256), 0, st, nz, O, V, acc, kx, out);
 }
+// Kx[(i,a),(j,b)] = Kx[(j,b),(i,a)] for the blocks build_kx left out: one 64 x 64 tile of
+// one block pair per 256-thread block, through LDS (reads along a of block (j, i), writes
+// along b of block (i, j), both coalesced)
+__global__ void __launch_bounds__(256) k_kx_mirror(int V, long ld, int i0, int fold, double* __restrict__ K) {
+  const int i = i0 + blockIdx.y, j = i0 + blockIdx.z;
+  const int ci = i0 + ((i - i0) / fold) * fold;
+  if (j >= ci) return;                         // built directly (or its own mirror source)
+  const int nt = (V + 63) / 64;
+  const int ta = blockIdx.x % nt, tb = blockIdx.x / nt;
+  __shared__ double s[64][65];
+  const int tid = threadIdx.x, cx = tid & 63, ry = tid >> 6;
+  const double* src = K + ((long)j * V) * ld + (long)i * V;   // block (j, i): row b, column a
+  double* dst = K + ((long)i * V) * ld + (long)j * V;         // block (i, j): row a, column b
+#pragma unroll 4
+  for (int r = 0; r < 16; ++r) {
+    const int b = tb * 64 + 4 * r + ry, a = ta * 64 + cx;
+    if (a < V && b < V) s[4 * r + ry][cx] = src[(long)b * ld + a];
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int r = 0; r < 16; ++r) {
+    const int a = ta * 64 + 4 * r + ry, b = tb * 64 + cx;
+    if (a < V && b < V) dst[(long)a * ld + b] = s[cx][4 * r + ry];
+  }
+}
+
+void kx_mirror(hipStream_t st, int O, int V, long ld, int i0, int i1, int fold, double* K) {
+  (void)O;
+  const int nt = (V + 63) / 64, n = i1 - i0;
+  if (n <= fold) return;                       // one chunk: every block built directly
+  hipLaunchKernelGGL(k_kx_mirror, dim3(nt * nt, n, n), dim3(256), 0, st, V, ld, i0, fold, K);
+}
+
 void permute_xi(hipStream_t st, int nz, int O, int V, const double* src, double* dst) {
   hipLaunchKernelGGL(k_permute_xi, dim3(nblocks((long)nz * O * V)), dim3(256), 0, st, nz, O, V, src, dst);
 }
