@@ -132,9 +132,13 @@ k_xc_rho_w(int O, int nx, int V, int n,
   const __amdgpu_buffer_rsrc_t wrs[3] = {rsrc_of(Wg + (long)g0 * wg), rsrc_of(Wg + wc + (long)g0 * wg),
                                          rsrc_of(Wg + 2 * wc + (long)g0 * wg)};
   double rw[W_LD];
-  auto load_w = [&](int at) XT_INLINE {
+  auto load_w1 = [&](int k, int at) XT_INLINE {   // k compile-time after unrolling
+    rw[k] = bld8(wrs[k / 4], w_off, (int)((16 * (k % 4) * wg + (long)at * WA) * 8));
+  };
+  auto load_w = [&](int k0, int at) XT_INLINE {
 #pragma unroll
-    for (int k = 0; k < W_LD; ++k) rw[k] = bld8(wrs[k / 4], w_off, (int)((16 * (k % 4) * wg + (long)at * WA) * 8));
+    for (int k = 0; k < W_LD; ++k)
+      if (k >= k0) load_w1(k, at);
   };
   double* const w_st = sW + wr * WP + wa;
   auto store_w = [&](auto BUF, int at) XT_INLINE {
@@ -148,7 +152,7 @@ k_xc_rho_w(int O, int nx, int V, int n,
       for (int k = 0; k < W_LD; ++k) w_st[B * W_IMG + ((k / 4) * GB + 16 * (k % 4)) * WP] = live ? rw[k] : 0.0;
     }
   };
-  load_w(0);
+  load_w(0, 0);
   store_w(std::integral_constant<int, 0>{}, 0);
 
   // ---- Zp ring: lane (q, r16) of k-step s supplies row i = 8 (s / 2) + 2 q + (s & 1)
@@ -212,15 +216,51 @@ k_xc_rho_w(int O, int nx, int V, int n,
   };
   using F = std::integral_constant<bool, false>;
   using T1 = std::integral_constant<bool, true>;
+  // kpair that also issues the next a-tile's weight loads K0 and K0 + 1, one before each
+  // k-step.  The 12 weight loads of an a-tile are spread over its first 12 k-steps: issued
+  // together at the tile start they queue ahead of the Zp ring's loads, and the ring's
+  // in-order vmcnt waits then stall on them (same box: 147.2 -> 142.8 ms per step; 4 / 2
+  // loads per k-step pair 144.8 / 143.3)
+  auto kpair_w = [&](auto SL, auto BB, auto ZERO, auto NT_, int pn, auto K0, bool wn, int at) XT_INLINE {
+    constexpr int sl = decltype(SL)::value, bb = decltype(BB)::value, k0 = decltype(K0)::value;
+    bread(pn, bq[bb ^ 1]);
+    if (wn) load_w1(k0, at);
+    step(std::integral_constant<int, sl>{}, BB, std::integral_constant<int, 0>{}, ZERO, NT_);
+    if (wn) load_w1(k0 + 1, at);
+    step(std::integral_constant<int, (sl + 1) % ZD>{}, BB, std::integral_constant<int, 1>{},
+         std::integral_constant<bool, false>{}, NT_);
+  };
+  using W0 = std::integral_constant<int, 0>;
+  using W2 = std::integral_constant<int, 2>;
+  using W4 = std::integral_constant<int, 4>;
+  using W6 = std::integral_constant<int, 6>;
+  using W8 = std::integral_constant<int, 8>;
+  using W10 = std::integral_constant<int, 10>;
 
   // one a-tile: ring phase P (slot of its first k-step), weight buffer BUF and live row
   // sub-tiles NT_ compile-time
   auto tile = [&](auto PH, auto BUF, auto NT_, int at) XT_INLINE {
     constexpr int P = decltype(PH)::value, B = decltype(BUF)::value, NTL = decltype(NT_)::value;
-    if (at + 1 < nat) load_w(at + 1);
+    using SA = std::integral_constant<int, P>;               // ring slots of even / odd pairs
+    using SB = std::integral_constant<int, (P + 2) % ZD>;
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    const bool wn = at + 1 < nat;
+    if (!wave_on && wn) load_w(0, at + 1);
     if (wave_on) {
-      kpair(std::integral_constant<int, P>{}, std::integral_constant<int, 0>{}, T1{}, NT_, p_lo + 1);
+      kpair_w(SA{}, B0{}, T1{}, NT_, p_lo + 1, W0{}, wn, at + 1);
       int k = 1;
+      if (np >= 7) {          // the first three pairs of k-step pairs peeled: weights 2 .. 11
+        kpair_w(SB{}, B1{}, F{}, NT_, p_lo + 2, W2{}, wn, at + 1);
+        kpair_w(SA{}, B0{}, F{}, NT_, p_lo + 3, W4{}, wn, at + 1);
+        kpair_w(SB{}, B1{}, F{}, NT_, p_lo + 4, W6{}, wn, at + 1);
+        kpair_w(SA{}, B0{}, F{}, NT_, p_lo + 5, W8{}, wn, at + 1);
+        kpair_w(SB{}, B1{}, F{}, NT_, p_lo + 6, W10{}, wn, at + 1);
+        kpair(SA{}, B0{}, F{}, NT_, p_lo + 7);
+        k = 7;
+      } else if (wn) {
+        load_w(2, at + 1);
+      }
       for (; k + 2 <= np; k += 2) {
         kpair(std::integral_constant<int, (P + 2) % ZD>{}, std::integral_constant<int, 1>{}, F{}, NT_, p_lo + k + 1);
         kpair(std::integral_constant<int, P>{}, std::integral_constant<int, 0>{}, F{}, NT_, p_lo + k + 2);
