@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 import pytest  # noqa: E402
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_bench_self_launches_ranks(world):
     env = dict(os.environ, XT_BENCH_BACKEND="gloo", XT_BENCH_OPERATOR="bench_stub:make_workload",
                PYTHONPATH=os.path.join(ROOT, "tests") + os.pathsep + ROOT, OMP_NUM_THREADS="1")
