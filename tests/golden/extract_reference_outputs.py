@@ -113,7 +113,17 @@ def main():
         out[f"{tag}_td_osc"] = rows[:, 2].tolist()
         if rows.shape[1] > 4:
             out[f"{tag}_td_delta_s2"] = rows[:, 4].tolist()
+        if cell == 6:   # xtda.analyze(): the spin-tensor (so2st) CI coefficients above 0.1
+            states = []
+            for line in log[log.index("D1 "):].splitlines():
+                f = line.split()
+                if f and re.fullmatch(r"D\d+", f[0]):
+                    states.append([])
+                elif len(f) >= 6 and f[0] in ("CV(0)", "OV(0)", "CO(0)", "CV(1)") and f[2] == "->":
+                    states[-1].append([f[0], int(f[1]), int(f[3]), float(f[5])])
+            out[f"{tag}_analyze"] = states
     assert len(out["ch2o_roks_b3lyp_td_ev"]) == 12 and len(out["ch2o_uks_b3lyp_td_ev"]) == 12
+    assert len(out["ch2o_roks_b3lyp_analyze"]) == 12
 
     assert len(out["xsf_roks_alda0_ev"]) == 10 and len(out["usf_uks_alda0_ev"]) == 10
     assert len(out["hf_631g_grid_ang_F"]) == 75 and len(out["hf_631g_grid_ang_H"]) == 50

@@ -136,6 +136,37 @@ def tda_meanfield(name: str):
     return tda_scf(name).to_meanfield()
 
 
+def analyze_mismatch(x, ref_states, tol=2e-4):
+    """Largest deviation between XTDA.analyze()'s spin-tensor coefficients (so2st of the
+    solver's eigenvectors, XTDA.py:893-937) and the reference's printed ones, in magnitude:
+    each MO's phase is arbitrary (the sign of an eigenvector of the Fock matrix), so the
+    relative signs of a state's coefficients over different orbitals are not comparable
+    between two SCF codes.  Every printed (block, i -> a, |c_i|) is looked up in our vector,
+    and our entries above the 0.1 print threshold (+ tol) must all be printed ones."""
+    import numpy as np
+    from xtddft_amd.utils import so2st
+    nc, no, nv = x.nc, x.no, x.nv
+    vv = so2st(x.v, nc, no, nv)
+    offs = {"CV(0)": (0, 0, nc + no, nv), "OV(0)": (nc * nv, nc, nc + no, nv),
+            "CO(0)": ((nc + no) * nv, 0, nc, no), "CV(1)": ((nc + no) * nv + nc * no, 0, nc + no, nv)}
+
+    def flat(tag, i, a):
+        base, oo, vo, width = offs[tag]
+        return base + (i - 1 - oo) * width + (a - 1 - vo)
+    worst = 0.0
+    for n, entries in enumerate(ref_states):
+        col = vv[:, n]
+        printed = set()
+        for tag, i, a, c in entries:
+            k = flat(tag, i, a)
+            printed.add(k)
+            worst = max(worst, abs(abs(col[k]) - abs(c)))
+        others = [k for k in np.where(np.abs(col) > 0.1 + tol)[0] if k not in printed]
+        if others:
+            worst = max(worst, float(np.abs(col[others]).max()))
+    return worst
+
+
 HF_POL_BASIS = None
 
 

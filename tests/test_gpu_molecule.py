@@ -108,6 +108,9 @@ def test_xtda_kernel_matches_reference_printout(torch, name, tag, jk_mode):
     if name.endswith("ROKS"):   # cell 4's Delta<S^2> is UTDA.py's UKS formula, not XTDA.py:831-836
         assert np.abs(x.dS2 - ref[f"{tag}_td_delta_s2"]).max() < tol
     assert np.abs(x.osc_str() - ref[f"{tag}_td_osc"]).max() < tol
+    if name.endswith("ROKS"):   # xtda.analyze()'s spin-tensor coefficients (XTDA.py:893-937)
+        from molecules import analyze_mismatch
+        assert analyze_mismatch(x, ref[f"{tag}_analyze"]) < 2e-4
 
 
 def test_utda_closed_shell_n2_contains_reference_tda_singlets(torch):

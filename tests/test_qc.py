@@ -166,6 +166,28 @@ def test_oracle_xtda_utda_roots_match_reference(name, tag):
     assert np.abs(w - ref).max() < TD_PRINT_TOL_EV, (w, ref)
 
 
+def test_oracle_xtda_analyze_coefficients_match_reference():
+    """XTDA.analyze (XTDA.py:893-937): the spin-tensor CI coefficients (so2st, utils.py) of
+    the 12 CH2O+ X-TDA states from the oracle's explicit-A eigenvectors against every
+    coefficient the reference printed (5 decimals, |c| > 0.1; TDA.ipynb cell 6), in magnitude
+    (MO phases are arbitrary)."""
+    from molecules import analyze_mismatch, tda_meanfield
+    from oracle import xtda as oxtda
+    from xtddft_amd import XTDA
+    from xtddft_amd.utils import order_pyscf2my
+    mf = tda_meanfield("CH2O_ROKS")
+    vind, hdiag = oxtda.gen_tda_operation(mf)
+    a = vind(np.eye(hdiag.size)).T
+    w, v = np.linalg.eigh(0.5 * (a + a.T))
+    keep = w > 1e-3
+    x = XTDA(mf.mol, mf, nstates=12)
+    info = mf.shape_info()
+    x.nc, x.no, x.nv = info["nc"], info["no"], info["nv"]
+    x.order = order_pyscf2my(x.nc, x.no, x.nv)
+    x.e, x.v = w[keep][:12], v[:, keep][:, :12][x.order]
+    assert analyze_mismatch(x, reference_outputs()["ch2o_roks_b3lyp_analyze"]) < 2e-4
+
+
 def test_oracle_utda_on_closed_shell_contains_tda_singlets():
     """N2 / B3LYP / cc-pVDZ (example/TDA.ipynb cell 2, closed-shell TDA singlets):
     U-TDA on the closed-shell UKS mean field spans singlets and triplets, so every
