@@ -165,3 +165,14 @@ def test_meanfield_eri_validation():
         dataclasses.replace(mf, eri=mf.eri[:-1])
     with pytest.raises(ValueError):
         dataclasses.replace(mf, eri=None)
+
+
+@pytest.mark.skipif(os.environ.get("XT_ASAN") != "1",
+                    reason="host AddressSanitizer build of the whole library takes ~3 min: XT_ASAN=1")
+def test_host_asan_build_of_the_c_abi():
+    """SURVEY.md section 5 (race detection / sanitizers): every csrc file built with
+    -Xarch_host -fsanitize=address, and tests/asan/asan_driver.cpp drives the C ABI's
+    validation and error paths under ASan (no GPU needed; tools/asan_host.sh)."""
+    r = subprocess.run(["bash", "tools/asan_host.sh"], cwd=ROOT, capture_output=True, text=True, timeout=1800)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "asan driver: ok" in r.stdout

@@ -955,8 +955,8 @@ void xc_uks_w(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O
     const dim3 grid((G + 3) / 4), blk(256);
 #define XT_POINT(NC, IC) hipLaunchKernelGGL((k_xc_point<NC, IC>), grid, blk, 0, st, G, g0, ngrid, nz, O, nmo, compP, \
                                             pO0, pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1)
-    if (ncomp == 4) { if (O <= 128) XT_POINT(4, 2); else XT_POINT(4, 4); }
-    else            { if (O <= 128) XT_POINT(1, 2); else XT_POINT(1, 4); }
+    if (ncomp == 4) { if (O <= 64) XT_POINT(4, 1); else if (O <= 128) XT_POINT(4, 2); else XT_POINT(4, 4); }
+    else            { if (O <= 64) XT_POINT(1, 1); else if (O <= 128) XT_POINT(1, 2); else XT_POINT(1, 4); }
 #undef XT_POINT
     return;
   }
