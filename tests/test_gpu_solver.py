@@ -67,6 +67,27 @@ def test_dgemm_strided_reduce_index(torch, hiplib, m, n, k, r, nb, ak, bk):
     assert float((c - ref).abs().max()) / scale < 1e-13 * (r * k) ** 0.5
 
 
+def test_davidson_checkpoint_and_restart(torch, tmp_path):
+    """davidson.checkpoint saves the Ritz vectors every iteration; a solve restarted from
+    the file (x0 = restart_guess) converges to the same roots in fewer iterations."""
+    from xtddft_amd import XTDA
+    from xtddft_amd.davidson import checkpoint, restart_guess
+    mf = make_mf(nao=40, nc=8, no=2, xctype="GGA", hyb=0.2)
+    path = str(tmp_path / "dav.npz")
+    x = XTDA(None, mf, nstates=6)
+    x.callback = checkpoint(path)
+    x.max_cycle = 4                       # interrupted before convergence
+    x.kernel()
+    x0, e_ck, icyc = restart_guess(path)
+    assert x0.shape == (6, x.operator().dim) and icyc >= 1
+    y = XTDA(None, mf, nstates=6)
+    e_full = y.kernel()
+    z = XTDA(None, mf, nstates=6)
+    e_re = z.Davidson(x0=x0)
+    assert np.all(z.converged) and np.abs(np.asarray(e_re) - np.asarray(e_full)).max() < 1e-9
+    assert z.icyc < y.icyc
+
+
 def test_davidson_matches_oracle_davidson(torch):
     from xtddft_amd.davidson import DiagPrecond, davidson1
     from xtddft_amd.operator import DeviceOperator

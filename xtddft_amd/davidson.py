@@ -209,6 +209,32 @@ def _sort_elast(elast, conv_last, vlast, v):
     return elast[mapidx], conv_last[mapidx]
 
 
+def checkpoint(path: str, every: int = 1):
+    """A ``davidson1`` callback that saves the current Ritz vectors, Ritz values, the
+    convergence flags and the iteration to ``path`` (NumPy ``.npz``, written to a temporary
+    file and renamed, so an interrupted write never leaves a torn file) every ``every``
+    iterations.  Resume with ``x0 = restart_guess(path)[0]`` (the reference Davidson takes
+    any x0, Davidson.py:21-298; SURVEY.md section 5 "checkpoint / resume")."""
+    import os
+
+    def cb(envs):
+        icyc = int(envs["icyc"])
+        if icyc % max(1, int(every)):
+            return
+        tmp = path + ".tmp"
+        with open(tmp, "wb") as fh:
+            np.savez(fh, x=envs["x0r"].cpu().numpy(), e=np.asarray(envs["e"]),
+                     conv=np.asarray(envs["conv"]), icyc=icyc)
+        os.replace(tmp, path)
+    return cb
+
+
+def restart_guess(path: str):
+    """(x0, e, icyc) from a ``checkpoint`` file (x0: Ritz vectors as rows)."""
+    with np.load(path) as f:
+        return f["x"], f["e"], int(f["icyc"])
+
+
 def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e-14,
               max_memory=4000, dot=None, callback=None, nroots=1, lessio=False, pick=None,
               verbose=None, follow_state=False, tol_residual=None, fill_heff=None, device=0,

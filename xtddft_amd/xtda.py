@@ -49,6 +49,7 @@ class XTDA:
             raise ValueError("mf must be a ROKS or UKS mean field")
         self.X = bool(mf.is_rohf)
         self._op = None
+        self.callback = None      # davidson1 callback, e.g. davidson.checkpoint(path)
 
     # ------------------------------------------------------------------ API
     def kernel(self):
@@ -130,7 +131,7 @@ class XTDA:
             x0 = self.get_init_guess(self.mf, nstates)
         self.converged, self.e, x1, self.icyc = _dav.davidson1(
             vind, x0, precond, tol_residual=self.conv_tol, lindep=self.lindep, nroots=nstates,
-            pick=pickeig, max_cycle=self.max_cycle, device=self.device)
+            pick=pickeig, max_cycle=self.max_cycle, device=self.device, callback=self.callback)
         info = self.mf.shape_info()
         nc, no, nv = info['nc'], info['no'], info['nv']
         v = np.asarray(x1).T
