@@ -555,7 +555,10 @@ def rank_main(args):
         if backend != "nccl":     # gloo rehearsal: ranks share the visible GPU(s)
             local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
-    if world > 1:
+    # XT_BENCH_FORCE_PG=1: a process group (and its collectives) even at world 1 -- the
+    # single-GPU pool's only way to run RCCL itself (two ranks on one GPU are refused)
+    pg = world > 1 or os.environ.get("XT_BENCH_FORCE_PG") == "1"
+    if pg:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
@@ -564,7 +567,7 @@ def rank_main(args):
         from xtddft_amd import build
         if rank == 0:
             build.build()
-        if world > 1:
+        if pg:
             dist.barrier()
     from xtddft_amd.parallel import allreduce_sigma
 
@@ -590,7 +593,7 @@ def rank_main(args):
         step()
     op.set_profile(0b111110)
     stats_acc = {}
-    if world > 1:
+    if pg:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
@@ -601,14 +604,14 @@ def rank_main(args):
             a["ms"] += s["ms"]; a["launches"] += s["launches"]; a["flops"] += s["flops"]
             a["bytes"] += s.get("bytes", 0.0)
     sync()
-    if world > 1:
+    if pg:
         dist.barrier()
     dt = time.perf_counter() - t0
     op.set_profile(0)
     # RCCL reduces device tensors only (a host tensor raises under the nccl backend)
     tt = torch.tensor([dt], dtype=torch.float64,
                       device=w.device if (use_gpu and backend == "nccl") else "cpu")
-    if world > 1:
+    if pg:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     T = float(tt.item())
     log(f"timed {args.steps} steps: {1e3 * T / args.steps:.2f} ms per step")
@@ -664,7 +667,7 @@ def rank_main(args):
     if use_gpu and (not args.no_converge or args.converge):
         result["converge"] = converge(args, w, allreduce_sigma)
         mine["converge"] = {k: result["converge"][k] for k in ("ax_s", "allreduce_s", "host_davidson_s")}
-    if world > 1:
+    if pg:
         ranks = [None] * world
         dist.all_gather_object(ranks, mine)
         result["ranks"] = ranks
@@ -672,7 +675,7 @@ def rank_main(args):
         result["ranks"] = [mine]
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
     return 0
 

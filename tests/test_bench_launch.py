@@ -52,3 +52,28 @@ def test_bench_two_ranks_on_the_gpu():
     assert d["n_gpus"] == 2 and d["value"] > 0 and "STUB" not in d["data"]
     assert "grid sharded x2" in d["config"]["parallelism"]
     assert len(d["ranks"]) == 2 and all(x["ax_ms"] > 0 for x in d["ranks"])
+
+
+@pytest.mark.gpu
+def test_bench_under_rccl_single_rank():
+    """RCCL itself on the one-GPU pool: the driver's launch line (torch.distributed.run)
+    at one rank with XT_BENCH_FORCE_PG=1, so bench.py initialises the nccl (= RCCL) group
+    with device_id, and runs its barriers, the max-over-ranks all-reduce of the timed
+    region on a device tensor, all_gather_object of the per-rank split and the group's
+    teardown -- every collective the 8-GPU run calls, on one rank."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, XT_BENCH_FORCE_PG="1", XT_BENCH_BACKEND="nccl")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--steps", "2", "--warmup", "1", "--config", "C1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["value"] > 0 and "STUB" not in d["data"]
+    assert len(d["ranks"]) == 1 and d["ranks"][0]["rank"] == 0 and d["ranks"][0]["ax_ms"] > 0
+    assert d["converge"]["converged"]

@@ -258,13 +258,23 @@ SkShape sk_shape(int M) {
 }
 }  // namespace
 
+// K splits: the grid (strips x splits blocks) runs in rounds of the chip's block slots,
+// so the split count is chosen for the fill of the last round (every block streams the
+// same bytes): the fewest splits whose fill is within 2 % of the best seen, up to 8 rounds
+// and >= 4 k-chunks per split.  (Slots + 1 blocks would leave one round to 22 blocks.)
 static int skinny_splits_m(int M, int N, int K) {
   const SkShape sh = sk_shape(M);
-  const int strips = (N + sh.bn - 1) / sh.bn;
-  int s = (sh.slots * 256 + strips - 1) / strips;        // >= the chip's block slots
-  const int max_s = (K + 4 * sh.bk - 1) / (4 * sh.bk);   // keep >= 4 chunks per split
-  if (s > max_s) s = max_s;
-  return s < 1 ? 1 : s;
+  const long strips = (N + sh.bn - 1) / sh.bn, slots = (long)sh.slots * 256;
+  const int max_s = (K + 4 * sh.bk - 1) / (4 * sh.bk);
+  int best = 1;
+  double fill = -1.0;
+  for (int s = 1; s <= max_s; ++s) {
+    const long blocks = strips * s, rounds = (blocks + slots - 1) / slots;
+    if (rounds > 8) break;
+    const double f = (double)blocks / (double)(rounds * slots);
+    if (f > fill + 0.02) { fill = f; best = s; }
+  }
+  return best;
 }
 
 int skinny_splits(int N, int K) { return skinny_splits_m(48, N, K); }
