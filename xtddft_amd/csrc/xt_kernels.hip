@@ -537,6 +537,191 @@ k_xc_point(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
   }
 }
 
+// Sum each of 32 per-lane values over the wave; value j ends in lanes 2 j and 2 j + 1
+// (the wave_sum_transpose halving steps carried down to offset 2, then one xor-1 add).
+// The offset 8 / 2 / 1 exchanges are DPP moves inside a 16-lane row (row_ror 8, quad_perm),
+// offset 4 a ds_bpermute.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+template <int O>
+__device__ __forceinline__ double xchg(double send) {
+  if constexpr (O == 8) return dpp_d<0x128>(send);                                 // row_ror:8
+  else if constexpr (O == 4) return __shfl_xor(send, 4);
+  else if constexpr (O == 2) return dpp_d<0x4E>(send);                             // quad_perm 2,3,0,1
+  else return dpp_d<0xB1>(send);                                                   // quad_perm 1,0,3,2
+}
+template <int N, int O>
+__device__ __forceinline__ void halve_xor(double (&v)[32], int lane) {
+  const bool up = lane & O;
+#pragma unroll
+  for (int k = 0; k < N / 2; ++k) {
+    const double send = up ? v[k] : v[k + N / 2];
+    const double keep = up ? v[k + N / 2] : v[k];
+    v[k] = keep + xchg<O>(send);
+  }
+}
+__device__ __forceinline__ double wave_sum_transpose32(double (&v)[32], int lane) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k) { swap_rows32(v[k], v[k + 16]); v[k] += v[k + 16]; }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { swap_rows16(v[k], v[k + 8]); v[k] += v[k + 8]; }
+  halve_xor<8, 8>(v, lane);
+  halve_xor<4, 4>(v, lane);
+  halve_xor<2, 2>(v, lane);
+  return v[0] + xchg<1>(v[0]);
+}
+
+// The grid point kernel with XB = 32 / NV trial vectors per reduction (NV = 2 NC values per
+// vector: spin x component): k_xc_point reduces the NV values of ONE vector per wave-wide
+// transpose and broadcasts them back with 2 NV readlanes, a dependency chain that leaves the
+// kernel issue- and latency-bound when O is small (C5: O = 37, 1030 SIMD cycles per vector
+// and point).  Here one transpose reduces the 32 values of XB vectors (value j = (xb, s, c) in
+// lanes 2 j, 2 j + 1), the w fxc contraction runs lane-parallel (lane j: column (s, c) of its
+// vector, the NV rho of that vector gathered through 256 B of LDS), and the wv values go back
+// to the occupied lanes through LDS broadcast reads.  Same arithmetic per (point, vector).
+// The next batch's U rows are loaded while this one is reduced.
+template <int NC, int IC>
+__global__ void __launch_bounds__(256)
+k_xc_point_b(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
+             const double* __restrict__ pO0, const double* __restrict__ pO1,
+             const double* __restrict__ wfxc,
+             double* __restrict__ U0, long ldU0, double* __restrict__ U1, long ldU1,
+             double* __restrict__ R0, long ldR0, double* __restrict__ R1, long ldR1) {
+  constexpr int NV = 2 * NC, XB = 32 / NV;
+  __shared__ __attribute__((aligned(16))) double sh[4][2][32];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int g = blockIdx.x * 4 + wid;
+  if (g >= G) return;   // whole waves only; the LDS slots are per wave
+  const long gg = g0 + g;
+  double* rs = sh[wid][0];
+  double* ws = sh[wid][1];
+  double ph[2][NC][IC];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const double* po = s ? pO1 : pO0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int m = 0; m < IC; ++m) {
+        const int i = lane + 64 * m;
+        ph[s][c][m] = i < O ? po[c * compP + gg * nmo + i] : 0.0;
+      }
+  }
+  // this lane's value j = lane >> 1 = (xb, sl, yl) after the reduction
+  const int j = lane >> 1, xbl = j / NV, kl = j % NV, sl = kl / NC, yl = kl % NC;
+  double fk[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int t = k / NC, yy = k % NC;
+    fk[k] = wfxc[(long)(((t * NC + yy) * 2 + sl) * NC + yl) * ngrid + gg];
+  }
+  double* Ub[2] = {U0 + g * ldU0, U1 + g * ldU1};
+  double* Rl = (NC > 1 && yl > 0) ? (sl ? R1 + g * ldR1 : R0 + g * ldR0) + yl - 1 : nullptr;
+  // batch loads: U rows of XB vectors (lanes over occupied), this lane's rhoW value.
+  // Branch-free: lanes past O and vectors past nz read a clamped (valid) element and
+  // keep zero.
+  const double* ul[2][IC];
+  bool iv[IC];
+#pragma unroll
+  for (int m = 0; m < IC; ++m) {
+    const int i = lane + 64 * m;
+    iv[m] = i < O;
+    ul[0][m] = Ub[0] + (i < O ? i : O - 1);
+    ul[1][m] = Ub[1] + (i < O ? i : O - 1);
+  }
+  const double* rl = Rl ? Rl : (R0 ? R0 + g * ldR0 : Ub[0]);
+  double un[XB][2][IC], rn;
+  auto load_b = [&](int x0, double (&ub)[XB][2][IC], double& rb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int xb = 0; xb < XB; ++xb) {
+      const int x = x0 + xb < nz ? x0 + xb : nz - 1;
+      const bool xv = x0 + xb < nz;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int m = 0; m < IC; ++m) {
+          const double t = ul[s][m][(long)x * O];
+          ub[xb][s][m] = (iv[m] && xv) ? t : 0.0;
+        }
+    }
+    rb = 0.0;
+    if constexpr (NC > 1) {
+      const int x = x0 + xbl < nz ? x0 + xbl : nz - 1;
+      const double t = rl[3 * x];
+      rb = (Rl && x0 + xbl < nz) ? t : 0.0;
+    }
+  };
+  auto body = [&](int x0, const double (&u)[XB][2][IC], double r) __attribute__((always_inline)) {
+    double v[32];
+#pragma unroll
+    for (int xb = 0; xb < XB; ++xb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          double a = 0.0;
+#pragma unroll
+          for (int m = 0; m < IC; ++m) a += u[xb][s][m] * ph[s][c][m];
+          v[xb * NV + s * NC + c] = a;
+        }
+    const double rho = wave_sum_transpose32(v, lane) + r;
+    if (!(lane & 1)) rs[j] = rho;
+    __builtin_amdgcn_wave_barrier();   // LDS is in order within a wave; no memory fence (it
+                                       // would wait for the next batch's loads)
+    double wl = 0.0;
+#pragma unroll
+    for (int k = 0; k < NV; k += 2) {
+      const double2 p = *(const double2*)(rs + xbl * NV + k);
+      wl += fk[k] * p.x + fk[k + 1] * p.y;
+    }
+    if (!(lane & 1)) ws[j] = wl;
+    if constexpr (NC > 1) {
+      if (Rl && !(lane & 1) && x0 + xbl < nz) Rl[3 * (x0 + xbl)] = wl;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int xb = 0; xb < XB; ++xb) {
+      double wv[NV];
+#pragma unroll
+      for (int k = 0; k < NV; k += 2) {
+        const double2 p = *(const double2*)(ws + xb * NV + k);
+        wv[k] = p.x; wv[k + 1] = p.y;
+      }
+      if (x0 + xb < nz) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int m = 0; m < IC; ++m) {
+            const int i = lane + 64 * m;
+            double l = 0.0;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) l += wv[s * NC + c] * ph[s][c][m];
+            if (i < O) Ub[s][(long)(x0 + xb) * O + i] = l;
+          }
+      }
+    }
+    // the next batch's LDS writes come after every lane's reads of this one
+    __builtin_amdgcn_wave_barrier();
+  };
+  load_b(0, un, rn);
+  for (int x0 = 0; x0 < nz; x0 += XB) {
+    double u[XB][2][IC];
+#pragma unroll
+    for (int xb = 0; xb < XB; ++xb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int m = 0; m < IC; ++m) u[xb][s][m] = un[xb][s][m];
+    const double r = rn;
+    if (x0 + XB < nz) load_b(x0 + XB, un, rn);
+    body(x0, u, r);
+  }
+}
+
 // ALDA0 spin-flip kernel (SF_TDA.py:90-160): rho1 = sum_i U0 PhiO, wv = rho1*fsf, S0 = wv*PhiO
 __global__ void __launch_bounds__(256)
 k_xc_sf(int G, int g0, int nz, int O, int nmo, const double* __restrict__ phio,
@@ -955,7 +1140,17 @@ void xc_uks_w(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O
     const dim3 grid((G + 3) / 4), blk(256);
 #define XT_POINT(NC, IC) hipLaunchKernelGGL((k_xc_point<NC, IC>), grid, blk, 0, st, G, g0, ngrid, nz, O, nmo, compP, \
                                             pO0, pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1)
-    if (ncomp == 4) { if (O <= 64) XT_POINT(4, 1); else if (O <= 128) XT_POINT(4, 2); else XT_POINT(4, 4); }
+    // GGA, O <= 128: several vectors per reduction (k_xc_point_b; same box: C5 18.5-18.6 ->
+    // 17.6-17.7 ms per A.x, C2 10.72-10.75 -> 10.17-10.26, headline neutral; two batches in
+    // flight or ds_bpermute instead of DPP: within 1 %)
+    if (ncomp == 4 && O <= 128) {
+      if (O <= 64) hipLaunchKernelGGL((k_xc_point_b<4, 1>), grid, blk, 0, st, G, g0, ngrid, nz, O, nmo, compP, pO0,
+                                      pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1);
+      else         hipLaunchKernelGGL((k_xc_point_b<4, 2>), grid, blk, 0, st, G, g0, ngrid, nz, O, nmo, compP, pO0,
+                                      pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1);
+      return;
+    }
+    if (ncomp == 4) XT_POINT(4, 4);
     else            { if (O <= 64) XT_POINT(1, 1); else if (O <= 128) XT_POINT(1, 2); else XT_POINT(1, 4); }
 #undef XT_POINT
     return;
