@@ -1136,6 +1136,7 @@ void xc_uks_mgga(hipStream_t st, int G, int g0, int ngrid, int nz, int O, int nm
 void xc_uks_w(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
               const double* pO0, const double* pO1, const double* wfxc, double* U0, long ldU0,
               double* U1, long ldU1, double* R0, long ldR0, double* R1, long ldR1) {
+  if (G <= 0 || nz <= 0 || O <= 0) return;
   if (O <= 256) {   // one wave per grid point, occupied values in registers
     const dim3 grid((G + 3) / 4), blk(256);
 #define XT_POINT(NC, IC) hipLaunchKernelGGL((k_xc_point<NC, IC>), grid, blk, 0, st, G, g0, ngrid, nz, O, nmo, compP, \
