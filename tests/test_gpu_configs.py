@@ -12,6 +12,8 @@ through the C ABI.
   compressed) at FULL size: symmetry, linearity and batch invariance of A, the
   reference drivers' Davidson converged for every root, and each root's
   residual |A v - w v| re-checked by a separate A.x call.
+* H, the headline shape (X-TDA, nao 1000, 20 roots, stored exchange) at FULL size: the
+  same properties, Davidson and residual checks.
 Tolerances: 1e-12 relative on sigma (FP64 round-off of a different summation
 order), 1e-9 Ha on Davidson-vs-Davidson / explicit-A eigenvalues.
 """
@@ -182,3 +184,23 @@ def test_c4_c60_xsf_full_size(torch, name, sa):
     r = _residuals(torch, x._op, np.asarray(x.e), v)
     assert r.max() < 1e-4, r           # XSF_TDA.py:1467 tol 1e-8 -> residual <= sqrt(tol)
     x._op.close()
+
+
+def test_h_headline_xtda_full_size(torch):
+    """The headline shape itself (bench config H: nao 1000, 101 / 99 occupied, naux 3000,
+    ngrid 1.2 M, GGA, the 62 GiB stored exchange): symmetry, linearity and batch
+    invariance of A, the 20-root X-TDA Davidson converged, and every root's residual
+    re-checked by a separate A.x (XTDA.py:769-777 criteria: |r| < 1e-5)."""
+    from xtddft_amd import XTDA
+    mf, c = _device_mf("H")
+    x = XTDA(None, mf, nstates=c["nroots"])
+    e = x.kernel()
+    op = x.operator()
+    assert op.k_mode == "stored"
+    _properties(torch, op)
+    assert np.all(x.converged) and len(e) == c["nroots"]
+    v = np.empty_like(x.v)
+    v[x.order] = x.v                                       # back to the operator's order
+    r = _residuals(torch, op, np.asarray(e), v)
+    assert r.max() < 1e-4, r
+    op.close()
