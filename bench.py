@@ -558,6 +558,15 @@ def rank_main(args):
     # XT_BENCH_FORCE_PG=1: a process group (and its collectives) even at world 1 -- the
     # single-GPU pool's only way to run RCCL itself (two ranks on one GPU are refused)
     pg = world > 1 or os.environ.get("XT_BENCH_FORCE_PG") == "1"
+    if world > 1:
+        # the host side of a rank (the replicated Davidson's subspace eigh, <= 108^2) is tiny:
+        # N ranks x the node's BLAS thread count oversubscribe the host (8 gloo ranks on one
+        # box: 0.8-1.5 s of host Davidson per solve against 0.07 s at N = 1)
+        try:
+            from threadpoolctl import threadpool_limits
+            threadpool_limits(limits=2)
+        except Exception:
+            pass
     if pg:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
