@@ -252,3 +252,32 @@ def test_eri8_sharded_cholesky_sums_to_full(dev):
     full = dev(mf, "XTDA").apply(z)
     parts = [dev(mf, "XTDA", shard=(r, 3)).apply(z) for r in range(3)]
     assert rel(sum(parts), full) < 1e-13
+
+
+def test_apply_boundary_checks(hiplib):
+    """DeviceOperator.apply at the C-ABI boundary: an empty batch returns an empty result
+    (host and device) without a launch; a zero vector maps to exactly zero; float32 input,
+    a wrong length, or an `out` of the wrong shape / dtype is refused before any kernel
+    could read or write past a buffer."""
+    import torch
+    from xtddft_amd.operator import DeviceOperator
+    mf = make_mf(nao=26, nc=5, no=2, xctype="GGA", hyb=0.2)
+    op = DeviceOperator(mf, "XTDA")
+    assert op.apply(np.zeros((0, op.dim))).shape == (0, op.dim)
+    z0 = torch.zeros((0, op.dim), dtype=torch.float64, device="cuda")
+    assert tuple(op.apply(z0).shape) == (0, op.dim)
+    zero = torch.zeros((2, op.dim), dtype=torch.float64, device="cuda")
+    assert float(op.apply(zero).abs().max()) == 0.0
+    z = torch.randn((3, op.dim), dtype=torch.float64, device="cuda")
+    with pytest.raises(TypeError):
+        op.apply(z.float())
+    with pytest.raises(ValueError):
+        op.apply(z[:, :-1])
+    with pytest.raises(ValueError):
+        op.apply(z, out=torch.empty((2, op.dim), dtype=torch.float64, device="cuda"))
+    with pytest.raises(ValueError):
+        op.apply(z, out=torch.empty((3, op.dim), dtype=torch.float32, device="cuda"))
+    out = torch.empty_like(z)
+    assert op.apply(z, out=out) is out
+    assert rel(out.cpu().numpy(), op.apply(z.cpu().numpy())) < 1e-14
+    op.close()

@@ -90,6 +90,7 @@ class DeviceOperator:
         naux = mf.naux
         ngrid = mf.grids.ngrid if (mf.grids is not None and mf.xctype != "HF") else 0
         self.shard = (rank, nranks)
+        self.device = int(device)
         if replicate_df is None:
             replicate_df = k_mode != "direct" and presharded is not True
         self.replicate_df = bool(replicate_df) and nranks > 1
@@ -241,23 +242,39 @@ class DeviceOperator:
         """sigma = A z for zs of shape (nz, dim) (NumPy or CUDA tensor)."""
         if _is_device(zs):
             torch = _torch()
+            # the C ABI takes raw FP64 pointers on this context's device: refuse anything
+            # else here rather than let the kernels read or write past a buffer
+            if zs.dtype != torch.float64:
+                raise TypeError(f"trial vectors must be float64, got {zs.dtype}")
+            if zs.device.index != self.device:
+                raise ValueError(f"trial vectors on cuda:{zs.device.index}, operator on cuda:{self.device}")
             z = zs.contiguous()
             if z.dim() == 1:
                 z = z[None]
+            if z.dim() != 2 or z.shape[1] != self.dim:
+                raise ValueError(f"trial vectors have shape {tuple(z.shape)}, expected (nz, {self.dim})")
             nz = z.shape[0]
-            if z.shape[1] != self.dim:
-                raise ValueError(f"trial vectors have length {z.shape[1]}, expected {self.dim}")
             if out is None:
                 out = torch.empty_like(z)
+            elif (out.dtype != torch.float64 or not out.is_cuda or out.device.index != self.device
+                  or tuple(out.shape) != tuple(z.shape) or not out.is_contiguous()):
+                raise ValueError(f"out must be a contiguous float64 tensor of shape {tuple(z.shape)} "
+                                 f"on cuda:{self.device}")
+            if nz == 0:
+                return out
             _capi.check(self._L.xt_apply(self._h, nz, z.data_ptr(), out.data_ptr(),
                                          _capi.XT_PTR_DEVICE), "xt_apply")
             return out
+        if out is not None:
+            raise ValueError("out is for device tensors; host arrays return a new array")
         z = np.ascontiguousarray(np.asarray(zs, dtype=np.float64))
         if z.ndim == 1:
             z = z[None]
-        if z.shape[1] != self.dim:
-            raise ValueError(f"trial vectors have length {z.shape[1]}, expected {self.dim}")
+        if z.ndim != 2 or z.shape[1] != self.dim:
+            raise ValueError(f"trial vectors have shape {z.shape}, expected (nz, {self.dim})")
         out = np.empty_like(z)
+        if z.shape[0] == 0:
+            return out
         _capi.check(self._L.xt_apply(self._h, z.shape[0], z.ctypes.data, out.ctypes.data,
                                      _capi.XT_PTR_HOST), "xt_apply")
         return out
