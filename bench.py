@@ -625,6 +625,18 @@ def rank_main(args):
     T = float(tt.item())
     log(f"timed {args.steps} steps: {1e3 * T / args.steps:.2f} ms per step")
     verify = w.verify(z, out) if hasattr(w, "verify") else None   # a workload's own self-check
+    # outside the timed region: A is symmetric, so <y, A x> = <A y, x> on the measured
+    # operator itself (two 2-vector A.x calls, all-reduced like the timed ones)
+    symmetry = None
+    if use_gpu:
+        import torch
+        gs = torch.Generator(device=w.device)
+        gs.manual_seed(7)
+        xv = torch.randn((2, op.dim), dtype=torch.float64, device=w.device, generator=gs)
+        yv = torch.randn((2, op.dim), dtype=torch.float64, device=w.device, generator=gs)
+        ax, ay = allreduce_sigma(op.apply(xv)), allreduce_sigma(op.apply(yv))
+        lhs, rhs = yv @ ax.T, ay @ xv.T
+        symmetry = float((lhs - rhs).abs().max() / lhs.abs().max())
     phases = op.last_timings()
     # per-rank breakdown (outside the timed region: synchronised after each phase)
     mine = breakdown(op, z, out, allreduce_sigma, sync, stats_acc, args.steps, rank, world)
@@ -668,6 +680,9 @@ def rank_main(args):
     )
     if verify is not None:
         result["verify"] = verify
+    if symmetry is not None:
+        result["check"] = dict(symmetry_rel=symmetry,
+                               what="max |<y,Ax> - <Ay,x>| / max |<y,Ax>| over 2 x 2 random vectors")
     if rank == 0 and world == 1 and use_gpu and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(args)
