@@ -288,6 +288,11 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
       if (wave_on) compute(BUF);
       __syncthreads();
     };
+    // the younger half of the 8 waves (two per SIMD) no longer loses VALU arbitration at each
+    // segment start (one static s_setprio, no flips): same box 141.30-141.49 -> 140.76-141.04
+    // ms per step (rho-forward: neutral, not applied there)
+    if constexpr (NW == 8)
+      if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
     int kt = kt0;
     for (; kt + 2 <= kt1; kt += 2) {
       tile(B0{}, kt);
