@@ -68,10 +68,13 @@ CONFIGS = {
     "C4": dict(nao=840, nc=179, no=3, kind="XSF", nvec=40, nroots=40, hyb=0.5, sa=3, remove=True),
     "C4d": dict(nao=840, nc=180, no=1, kind="XSF", nvec=40, nroots=40, hyb=0.5, sa=0, remove=True),
     "C5": dict(nao=152, nc=35, no=2, kind="XTDA", nvec=50, nroots=50, hyb=0.2, jk="ERI8"),
+    # C3 with the multicollinear spin-flip kernel (method=1, SF_TDA.py:855-1047)
+    "C3mc": dict(nao=861, nc=91, no=4, kind="SF_UP", nvec=30, nroots=30, hyb=0.5, method=1),
 }
 CONFIG_NAMES = {"H": "headline", "C1": "CH2 triplet / 6-31G", "C2": "naphthalene+ / def2-SVP",
                 "C3": "Fe(II)P quintet / def2-TZVP", "C4": "C60-like quartet / def2-SVP",
-                "C4d": "C60- doublet / def2-SVP", "C5": "[Cu2O2]2+ triplet / def2-TZVP"}
+                "C4d": "C60- doublet / def2-SVP", "C5": "[Cu2O2]2+ triplet / def2-TZVP",
+                "C3mc": "Fe(II)P quintet / def2-TZVP, multicollinear kernel"}
 
 
 def parse(argv=None):
@@ -95,18 +98,20 @@ def parse(argv=None):
     ap.add_argument("--kind", default=None, choices=["XTDA", "SF_UP", "SF_DOWN", "XSF"])
     ap.add_argument("--sa", type=int, default=None, help="XSF spin-adaptation level (XSF_TDA.py SA)")
     ap.add_argument("--jk", default=None, choices=["DF", "ERI8"])
+    ap.add_argument("--method", type=int, default=None, choices=[0, 1],
+                    help="spin-flip XC kernel: 0 ALDA0, 1 multicollinear (SF / XSF kinds)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-converge", action="store_true")
     ap.add_argument("--converge", action="store_true", help="force the Davidson run (default on; see --no-converge)")
     ap.add_argument("--k-mode", default="auto", choices=["auto", "direct", "stored"],
                     help="exchange evaluation (xt_set_exchange_mode)")
     args = ap.parse_args(argv)
-    preset = dict(sa=0, remove=False, jk="DF", ngrid=None)
+    preset = dict(sa=0, remove=False, jk="DF", ngrid=None, method=0)
     preset.update(CONFIGS[args.config])
     # a shape overridden on the command line is not the profiled preset: its PMC
     # bytes (roofline.traffic) are unmeasured
     args.custom = any(getattr(args, k, None) is not None
-                      for k in ("nao", "nc", "no", "naux", "ngrid", "nvec", "hyb", "kind", "sa", "jk"))
+                      for k in ("nao", "nc", "no", "naux", "ngrid", "nvec", "hyb", "kind", "sa", "jk", "method"))
     for k, v in preset.items():
         if getattr(args, k, None) is None:
             setattr(args, k, v)
@@ -140,11 +145,14 @@ def launch(args, argv):
 class Workload:
     """What a factory returns: the operator, its mean field, the torch device the
     trial vectors live on, and the setup split (synthetic generation vs operator
-    construction = MO transforms + xt_prepare)."""
+    construction = MO transforms + xt_prepare).  ``regen()`` (device workloads) returns
+    the operator's input mean field again, bit-identical (same block seeds): what the
+    cpu_baseline leg hands the oracle."""
 
-    def __init__(self, op, mf, device, t_gen, t_op, replicate):
+    def __init__(self, op, mf, device, t_gen, t_op, replicate, regen=None):
         self.op, self.mf, self.device = op, mf, device
         self.t_gen, self.t_op, self.replicate = t_gen, t_op, replicate
+        self.regen = regen
 
 
 def _eri8_from_device_factor(cderi):
@@ -167,9 +175,10 @@ def device_workload(args, rank, world, local):
     replicate = world > 1 and args.k_mode != "direct"
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    mf = make_device_mf(nao=args.nao, nc=args.nc, no=args.no, naux=args.naux, ngrid=args.ngrid,
-                        xctype=args.xc, hyb=args.hyb, device=local, shard=(rank, world),
-                        full_aux=replicate or args.jk == "ERI8")
+    gen_kw = dict(nao=args.nao, nc=args.nc, no=args.no, naux=args.naux, ngrid=args.ngrid,
+                  xctype=args.xc, hyb=args.hyb, device=local, shard=(rank, world),
+                  full_aux=replicate or args.jk == "ERI8", sf_mc=args.method == 1)
+    mf = make_device_mf(**gen_kw)
     if args.jk == "ERI8":
         mf.eri = _eri8_from_device_factor(mf.cderi)
         mf.cderi = None
@@ -181,6 +190,8 @@ def device_workload(args, rank, world, local):
         # XSF_TDA.kernel default fglobal = (1 - d_lda) c_x + d_lda, d_lda = 0.3, c_x = hyb
         kw = dict(sa=args.sa, fglobal=0.7 * args.hyb + 0.3, foo=1.0, remove=bool(args.remove))
     t1 = time.perf_counter()
+    if args.method == 1:
+        kw.update(sf_kernel="mc", mc_kernel=mf.fxc_sf_mc)
     op = DeviceOperator(mf, args.kind, shard=(rank, world), device=local, **kw,
                         presharded="grid" if (replicate or args.jk == "ERI8") else True,
                         k_mode=args.k_mode, replicate_df=replicate)
@@ -193,8 +204,10 @@ def device_workload(args, rank, world, local):
     mf.grids = None
     mf.fxc = None
     mf.fxc_sf = None
+    mf.fxc_sf_mc = None
     torch.cuda.empty_cache()
-    return Workload(op, mf, torch.device(f"cuda:{local}"), t_gen, t_op, replicate)
+    return Workload(op, mf, torch.device(f"cuda:{local}"), t_gen, t_op, replicate,
+                    regen=lambda: make_device_mf(**gen_kw))
 
 
 def _factory():
@@ -251,8 +264,8 @@ def _oracle_vind(args, mf):
     if args.kind == "XTDA":
         return oxtda.gen_tda_operation(mf)
     if args.kind in ("SF_UP", "SF_DOWN"):
-        return osf.gen_tda_operation_sf(mf, 1 if args.kind == "SF_UP" else -1)
-    o = oxsf.XSFOracle(mf, SA=args.sa)
+        return osf.gen_tda_operation_sf(mf, 1 if args.kind == "SF_UP" else -1, method=args.method)
+    o = oxsf.XSFOracle(mf, SA=args.sa, method=args.method)
     o.re = bool(args.remove)
     if o.re and o.no > 1:
         o.vects = oxsf.get_vect(o.no)
@@ -278,50 +291,54 @@ def _time_call(f, reps, what=""):
     return float(np.median(ts))
 
 
-class _CyclicGrid:
-    """Full-size grid data for the oracle, streamed: the oracle walks the grid in
-    blocks of oracle.engines.GRID_BLOCK points (ao[:ncomp, g0:g1], weights[g0:g1],
-    fxc[..., g0:g1]); block b is served from stored block b mod nb.  The BLAS work
-    per block depends on the shape, not the values, so the timing is that of the
-    full grid without its 38 GB of AO values in host memory."""
+class _DevSlicer:
+    """A device tensor the oracle reads block by block: ``x[key]`` copies that block to
+    host memory (the oracle walks the grid in oracle.engines.GRID_BLOCK-point blocks), so
+    the full-size grid data never has to fit in host memory at once."""
 
-    class _View:
-        def __init__(self, blocks, axis_last, ngrid, gb):
-            self.blocks, self.ngrid, self.gb = blocks, ngrid, gb
+    def __init__(self, t):
+        self.t, self.shape = t, tuple(t.shape)
 
-        def __getitem__(self, key):
-            key = key if isinstance(key, tuple) else (key,)
-            sl = key[-1]
-            g0, g1 = sl.start or 0, self.ngrid if sl.stop is None else min(sl.stop, self.ngrid)
-            b = self.blocks[(g0 // self.gb) % len(self.blocks)]
-            return b[key[:-1] + (slice(0, g1 - g0),)]
-
-    def __init__(self, ao_blocks, w_blocks, ngrid, gb):
-        self.ao = self._View(ao_blocks, True, ngrid, gb)
-        self.weights = self._View(w_blocks, True, ngrid, gb)
-        self._ngrid = ngrid
-
-    @property
-    def ngrid(self):
-        return self._ngrid
+    def __getitem__(self, key):
+        return self.t[key].cpu().numpy()
 
 
-def cpu_baseline(args):
-    """The oracle's A.x (the reference's AO-route algorithm, NumPy/BLAS) on ALL
-    host cores, one trial vector per call.
-
-    Threads: every CPU this process may run on (``cpu_share``: the host's CPUs
-    capped by the cgroup quota of a shared GPU box; more BLAS threads than the
-    quota only oversubscribe it).  Shapes whose AO grid data stay small are timed
-    at the full (naux, ngrid), 1 warm-up + median of 5.  The large ones are timed
-    as ONE call at the full naux and the full ngrid (after a warm-up call of the
-    same vind at a small size): the DF factor is a small factor tiled to naux and
-    the grid is streamed block by block from a few stored blocks (``_CyclicGrid``),
-    so nothing is extrapolated.  The exact-K configuration contracts stored 4-index
-    ERIs (the incore mf._eri route), built from the same factor.  Returns matvecs/s."""
+def oracle_meanfield(args, w):
+    """The timed operator's own input data for the oracle: the workload's synthetic mean
+    field regenerated bit-identically on the device (``Workload.regen``: same seeds, same
+    block generators), the DF factor (or the stored ERIs it defines) copied to host
+    memory, the grid data copied too when small, else read from HBM block by block."""
     import dataclasses
+    from oracle.engines import eri_full_from_cderi
+    from xtddft_amd.meanfield import Grid
+    mf = w.regen()
+    cd = mf.cderi.cpu().numpy()
+    small = 8.0 * 4 * args.ngrid * args.nao < 4e9
+    conv = (lambda t: None if t is None else t.cpu().numpy()) if small else \
+        (lambda t: None if t is None else _DevSlicer(t))
+    grid = Grid(ao=conv(mf.grids.ao), weights=conv(mf.grids.weights))
+    out = dataclasses.replace(mf, cderi=cd, grids=grid, fxc=conv(mf.fxc), fxc_sf=conv(mf.fxc_sf),
+                              fxc_sf_mc=conv(mf.fxc_sf_mc), extra=dict(mf.extra))
+    if args.jk == "ERI8":
+        out.extra["eri_full"] = eri_full_from_cderi(cd)
+    return out, small
+
+
+def cpu_baseline(args, w, z0, s0):
+    """The oracle's A.x (the reference's AO-route algorithm, NumPy/BLAS) on ALL host
+    cores, on the SAME data and the SAME trial vector as the timed device steps.
+
+    Threads: every CPU this process may run on (``cpu_share``: the host's CPUs capped by
+    the cgroup quota of a shared GPU box; more BLAS threads than the quota only
+    oversubscribe it).  Data: ``oracle_meanfield`` (the timed operator's inputs).  Shapes
+    whose grid data fit host memory comfortably are timed 1 warm-up + median of 5; the
+    large ones as ONE call at the full naux and ngrid (after a warm-up call on a small
+    synthetic problem), the grid streamed from HBM block by block -- nothing extrapolated.
+    The exact-K configuration contracts stored 4-index ERIs (the incore mf._eri route).
+    Returns (cpu_baseline dict in matvecs/s, verify dict): ``verify.rel_err`` = max |sigma_gpu
+    - sigma_oracle| / max |sigma_oracle| for the first vector of the timed batch."""
     from threadpoolctl import threadpool_info, threadpool_limits
-    from oracle.engines import GRID_BLOCK, eri_full_from_cderi
+    from oracle.engines import GRID_BLOCK
     from xtddft_amd.synthetic import make_mf, make_trial_vectors
     ncpu = cpu_share()
     t_all = time.perf_counter()
@@ -330,55 +347,48 @@ def cpu_baseline(args):
                        if i.get("user_api") == "blas"] or [1])
         log(f"cpu baseline on {threads} BLAS threads ({ncpu} CPUs in this process's share, "
             f"{os.cpu_count()} on the host)")
+        t0 = time.perf_counter()
+        mfo, small = oracle_meanfield(args, w)
+        log(f"cpu baseline: the timed operator's data regenerated and staged in {time.perf_counter() - t0:.1f} s")
+        vind, _ = _oracle_vind(args, mfo)
+        res = {}
 
-        def build(naux, ngrid):
-            mf = make_mf(nao=args.nao, nc=args.nc, no=args.no, naux=naux, ngrid=ngrid,
-                         xctype=args.xc, hyb=args.hyb)
-            if args.jk == "ERI8":
-                mf = dataclasses.replace(mf, extra=dict(eri_full=eri_full_from_cderi(mf.cderi)))
-            return mf
-
-        def t_vec(mf, reps, what):
-            vind, hdiag = _oracle_vind(args, mf)
-            z = make_trial_vectors(1, hdiag.size)
-            return _time_call(lambda: vind(z), reps, what)
-        full = 8.0 * 4 * args.ngrid * args.nao < 4e9
-        if full:
-            t = t_vec(build(args.naux, args.ngrid), 5, "full size")
+        def call():
+            res["s"] = vind(z0)
+        if small:
+            t = _time_call(call, 5, "full size")
             how = f"timed at the full size (naux={args.naux}, ngrid={args.ngrid}), 1 warm-up + median of 5"
         else:
-            n_small, nblk = 16, 2
-            small = build(n_small, nblk * GRID_BLOCK)
-            # full-naux factor: the small factor tiled (the BLAS work depends on the
-            # shape, not the values; avoids generating 8 naux nao^2 bytes of normals)
-            reps_ = -(-args.naux // n_small)
-            ao, w = small.grids.ao, small.grids.weights
-            blocks = [slice(b * GRID_BLOCK, (b + 1) * GRID_BLOCK) for b in range(nblk)]
-            grid = _CyclicGrid([ao[:, b] for b in blocks], [w[b] for b in blocks], args.ngrid, GRID_BLOCK)
-            fxc = _CyclicGrid._View([small.fxc[..., b] for b in blocks], True, args.ngrid, GRID_BLOCK)
-            fsf = _CyclicGrid._View([small.fxc_sf[b] for b in blocks], True, args.ngrid, GRID_BLOCK)
-            big = dataclasses.replace(small, cderi=np.tile(small.cderi, (reps_, 1, 1))[:args.naux]
-                                      * np.sqrt(n_small / args.naux), grids=grid, fxc=fxc, fxc_sf=fsf)
-            vind_s, hd = _oracle_vind(args, small)
+            warm = make_mf(nao=args.nao, nc=args.nc, no=args.no, naux=16, ngrid=2 * GRID_BLOCK,
+                           xctype=args.xc, hyb=args.hyb)
+            vind_s, hd = _oracle_vind(args, warm)
             t0 = time.perf_counter()
             vind_s(make_trial_vectors(1, hd.size))          # warms BLAS threads and allocators
-            log(f"cpu baseline warm-up (naux={n_small}, ngrid={nblk * GRID_BLOCK}): "
-                f"{time.perf_counter() - t0:.2f} s")
-            vind_b, _ = _oracle_vind(args, big)
-            z1 = make_trial_vectors(1, hd.size)
-            log(f"cpu baseline: one call at naux={args.naux}, ngrid={args.ngrid} (streamed grid)")
+            log(f"cpu baseline warm-up (naux=16, ngrid={2 * GRID_BLOCK}): {time.perf_counter() - t0:.2f} s")
+            log(f"cpu baseline: one call at naux={args.naux}, ngrid={args.ngrid} (grid read from HBM)")
             t0 = time.perf_counter()
-            vind_b(z1)
+            call()
             t = time.perf_counter() - t0
             log(f"cpu baseline naux={args.naux} ngrid={args.ngrid}: {t:.2f} s")
-            how = (f"one call timed at the full naux={args.naux} and the full ngrid={args.ngrid} (grid streamed "
-                   f"in {GRID_BLOCK}-point blocks cycling {nblk} stored blocks, the DF factor tiled from "
-                   f"{n_small} functions), after a warm-up call at naux={n_small}, ngrid={nblk * GRID_BLOCK}")
-    return dict(value=1.0 / t, unit="matvecs/s", cores=int(threads), kind="port",
-                sample=(f"oracle {KIND_NAME[args.kind]} vind (NumPy AO route, "
-                        f"{'stored 4-index ERI' if args.jk == 'ERI8' else 'DF'} J/K, {args.xc}) on 1 vector "
-                        f"at nao={args.nao}: {how}; t_vec = {t:.2f} s"),
-                host=_host_info(), sample_wall_s=round(time.perf_counter() - t_all, 1))
+            how = (f"one call timed at the full naux={args.naux} and the full ngrid={args.ngrid} (the grid "
+                   f"data read from HBM in {GRID_BLOCK}-point blocks, included), after a warm-up call on "
+                   f"a small synthetic problem")
+    s_or = np.asarray(res["s"]).reshape(s0.shape)
+    err = float(np.abs(s0 - s_or).max() / np.abs(s_or).max())
+    log(f"verify: max |sigma_gpu - sigma_oracle| / max |sigma_oracle| = {err:.3e}")
+    del mfo
+    import torch
+    torch.cuda.empty_cache()
+    cpu = dict(value=1.0 / t, unit="matvecs/s", cores=int(threads), kind="port",
+               sample=(f"oracle {KIND_NAME[args.kind]} vind (NumPy AO route, "
+                       f"{'stored 4-index ERI' if args.jk == 'ERI8' else 'DF'} J/K, {args.xc}) on 1 vector "
+                       f"at nao={args.nao} on the timed operator's own data: {how}; t_vec = {t:.2f} s"),
+               host=_host_info(), sample_wall_s=round(time.perf_counter() - t_all, 1))
+    verify = dict(rel_err=err, max_abs_sigma=float(np.abs(s_or).max()),
+                  what=("max |sigma_gpu - sigma_oracle| / max |sigma_oracle| on the first vector of the timed "
+                        "batch, full naux and ngrid, the oracle (reference AO route) on the same data"),
+                  tol=1e-12, ok=bool(err <= 1e-12))
+    return cpu, verify
 
 
 # ---------------------------------------------------------------------------
@@ -617,6 +627,10 @@ def rank_main(args):
         dist.barrier()
     dt = time.perf_counter() - t0
     op.set_profile(0)
+    phases = op.last_timings()          # the last timed step's phase split
+    z0 = s0 = None
+    if use_gpu:                          # the first timed vector and its device sigma (verify)
+        z0, s0 = z[:1].cpu().numpy(), out[:1].cpu().numpy()
     # RCCL reduces device tensors only (a host tensor raises under the nccl backend)
     tt = torch.tensor([dt], dtype=torch.float64,
                       device=w.device if (use_gpu and backend == "nccl") else "cpu")
@@ -637,7 +651,6 @@ def rank_main(args):
         ax, ay = allreduce_sigma(op.apply(xv)), allreduce_sigma(op.apply(yv))
         lhs, rhs = yv @ ax.T, ay @ xv.T
         symmetry = float((lhs - rhs).abs().max() / lhs.abs().max())
-    phases = op.last_timings()
     # per-rank breakdown (outside the timed region: synchronised after each phase)
     mine = breakdown(op, z, out, allreduce_sigma, sync, stats_acc, args.steps, rank, world)
     roofline = roofline_of(args, stats_acc, args.steps, world)
@@ -655,13 +668,16 @@ def rank_main(args):
     workload = (f"{KIND_NAME[args.kind]} A.x, nao={args.nao}, nocc_a/nocc_b={args.nc + args.no}/{args.nc}, "
                 f"dim={op.dim}, nvec={args.nvec}, {args.jk} naux={args.naux}, ngrid={args.ngrid}, "
                 f"xc={args.xc}, hyb={args.hyb}"
+                + (", multicollinear kernel (method=1)" if args.method == 1 else "")
                 + (f", SA={args.sa}, remove={bool(args.remove)}" if args.kind == "XSF" else "")
                 + f" [BASELINE {args.config}: {CONFIG_NAMES[args.config]}]")
+    # a gloo rehearsal time-shares the visible GPU(s): n_gpus is the physical count
+    ngpu = world if (backend == "nccl" or not use_gpu) else min(world, torch.cuda.device_count())
     result = dict(
         metric="A·x matvecs/sec (nao, nocc×nvir, nvec)",
         value=round(args.nvec * args.steps / T, 4),
         unit="matvecs/s",
-        n_gpus=world, steps=args.steps, warmup=args.warmup,
+        n_gpus=ngpu, steps=args.steps, warmup=args.warmup,
         ms_per_step=round(1e3 * T / args.steps, 3),
         higher_is_better=True, scaling="strong", vs_baseline=None, dtype="f64",
         data=("synthetic (seeded ROKS mean field, DF factor, GGA grid kernel; generated in HBM)"
@@ -680,12 +696,15 @@ def rank_main(args):
     )
     if verify is not None:
         result["verify"] = verify
+    if ngpu != world:
+        result["rehearsal"] = (f"{world} ranks over {backend} time-sharing {ngpu} GPU(s): a correctness "
+                               f"rehearsal of the sharded path, not a {world}-GPU measurement")
     if symmetry is not None:
         result["check"] = dict(symmetry_rel=symmetry,
                                what="max |<y,Ax> - <Ay,x>| / max |<y,Ax>| over 2 x 2 random vectors")
     if rank == 0 and world == 1 and use_gpu and not args.no_cpu_baseline:
         try:
-            result["cpu_baseline"] = cpu_baseline(args)
+            result["cpu_baseline"], result["verify"] = cpu_baseline(args, w, z0, s0)
         except Exception as e:   # report, never hide
             result["cpu_baseline"] = dict(value=None, error=repr(e))
     if use_gpu and (not args.no_converge or args.converge):

@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define XT_ABI_VERSION 5
+#define XT_ABI_VERSION 6
 
 #define XT_PTR_HOST 0
 #define XT_PTR_DEVICE 1
@@ -32,6 +32,11 @@ extern "C" {
 #define XT_XC_LDA 1
 #define XT_XC_GGA 2
 #define XT_XC_MGGA 3       /* meta-GGA: (rho, grad rho, tau) kernel, XTDA.py:239-276 / nr_uks_fxc   */
+
+/* spin-flip XC kernels (SF_DOWN / SF_UP / XSF; the reference's `method`) */
+#define XT_SF_ALDA0 0      /* method 0: collinear-limit ALDA0, density only (SF_TDA.py:39-160)     */
+#define XT_SF_MC 1         /* method 1: multicollinear kernel over (s, grad s[, tau_s])            */
+                           /*   (_gen_uhf_tda_response_sf / nr_uks_fxc_sf_tda_mc, SF_TDA.py:855-1047) */
 
 typedef struct xt_ctx xt_ctx;
 
@@ -53,6 +58,7 @@ typedef struct xt_desc {
   int add_local;     /* 1: add the rank-local one-electron terms (Fock, Delta-A Fock
                         parts); set on exactly one rank of a sharded operator */
   int device;        /* HIP device ordinal */
+  int sf_kernel;     /* spin-flip kinds: XT_SF_ALDA0 or XT_SF_MC (ignored otherwise) */
 } xt_desc;
 
 /* lifetime ------------------------------------------------------------- */
@@ -100,13 +106,15 @@ int xt_set_jk_eri8(xt_ctx* ctx, const double* eri_s8, int which, double tol,
    found by xt_set_jk_eri8) and the full Cholesky rank of the last
    xt_set_jk_eri8 (before sharding). */
 int xt_naux(const xt_ctx* ctx, int* naux_local, int* chol_rank);
-/* AO values on the grid (ncomp x ngrid x nao; ncomp = 1 LDA / 4 GGA and MGGA),
-   weights (ngrid) and the kernel: UKS fxc (2 x nk x 2 x nk x ngrid, un-weighted;
-   nk = 1 LDA, 4 GGA, 5 MGGA with tau = 1/2 sum |grad phi|^2 last) for XTDA/UTDA, or
-   the weighted ALDA0 kernel (ngrid) for SF/XSF.
-   Replaces ni.cache_xc_kernel / cache_xc_kernel_sf (XTDA.py:504, SF_TDA.py:39-88)
-   and the per-call grid loop of ni.nr_uks_fxc / nr_uks_fxc_sf_tda
-   (XTDA.py:514, SF_TDA.py:90-160). */
+/* AO values on the grid (ncomp x ngrid x nao; ncomp = 1 LDA / 4 GGA and MGGA;
+   spin-flip ALDA0: 1), weights (ngrid) and the kernel: UKS fxc (2 x nk x 2 x nk x ngrid,
+   un-weighted; nk = 1 LDA, 4 GGA, 5 MGGA with tau = 1/2 sum |grad phi|^2 last) for
+   XTDA/UTDA; for SF/XSF the weighted ALDA0 kernel (ngrid), or with XT_SF_MC the
+   un-weighted multicollinear kernel fxc_sf (nk x nk x ngrid, the output of mcfun's
+   eval_xc_eff_sf; the library applies the reference's factor 2 and the weights).
+   Replaces ni.cache_xc_kernel / cache_xc_kernel_sf / cache_xc_kernel_sf_mc
+   (XTDA.py:504, SF_TDA.py:39-88, 942-974) and the per-call grid loop of ni.nr_uks_fxc /
+   nr_uks_fxc_sf_tda / nr_uks_fxc_sf_tda_mc (XTDA.py:514, SF_TDA.py:90-160, 976-1047). */
 int xt_set_grid(xt_ctx* ctx, const double* ao, const double* weights,
                 const double* kernel, int ptr_kind);
 /* XSF only: OO compression basis vects (no^2 x (no^2-1)) (XSF_TDA.py:397-414). */

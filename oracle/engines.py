@@ -234,13 +234,21 @@ def gen_response(mf, with_j=True):
 
 
 def gen_response_sf(mf, method=0):
-    """Restates SF_TDA.gen_response_sf (SF_TDA.py:246-286): no J in spin flip."""
+    """Restates SF_TDA.gen_response_sf (SF_TDA.py:246-286): no J in spin flip.
+    method 1: the multicollinear response of _gen_uhf_tda_response_sf (SF_TDA.py:855-904)
+    with the kernel mf.fxc_sf_mc (oracle.mcol.cache_xc_kernel_sf_mc)."""
+    if method == 1 and mf.xctype != 'HF' and mf.fxc_sf_mc is None:
+        raise ValueError("method 1 needs mf.fxc_sf_mc (the multicollinear kernel)")
+
     def vind(dm1):
         dm1 = np.asarray(dm1, dtype=np.float64)
         if mf.xctype == 'HF':
             return -jk(mf, dm1, with_j=False)[1]
         if method == 0:
             v1 = nr_uks_fxc_sf_tda(mf, dm1)
+        elif method == 1:
+            from .mcol import nr_uks_fxc_sf_tda_mc
+            v1 = nr_uks_fxc_sf_tda_mc(mf, mf.fxc_sf_mc, dm1)
         else:
             v1 = np.zeros_like(dm1)
         hybrid = (mf.hyb != 0) or (mf.omega != 0)

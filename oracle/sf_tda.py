@@ -5,7 +5,8 @@
 * ``amat_down`` / ``amat_up`` restate the explicit matrices of
   ``SF_TDA_down.get_Amat`` (SF_TDA.py:624-804) and ``SF_TDA_up.get_Amat``
   (SF_TDA.py:448-560) using MO integrals from the same DF factor and the
-  ALDA0 kernel ``fxc_sf`` on the grid.
+  ALDA0 kernel ``fxc_sf`` on the grid; ``method=1`` swaps in the multicollinear
+  block of ``get_ab_sf`` (SF_TDA.py:1051-1276, ``oracle.mcol``).
 """
 from __future__ import annotations
 
@@ -48,8 +49,6 @@ def gen_tda_operation_sf(mf, isf, method=0):
         ndim = (noccb, nvira)
         orbo, orbv = orbob, orbva
     hdiag = e_ia.ravel()
-    if method == 1:
-        raise NotImplementedError("multicollinear kernel needs mcfun (out of scope)")
     vresp = engines.gen_response_sf(mf, method=method)
 
     def vind(zs0):
@@ -89,10 +88,14 @@ def init_guess(mf, nstates, isf=-1):
     return x0
 
 
-def _sf_xc_kernel_block(mf, orbo, orbv):
-    """sum_g fxc_sf(g) (phi_o phi_v)(phi_o phi_v) over the grid (SF_TDA.py:509-556)."""
+def _sf_xc_kernel_block(mf, orbo, orbv, method=0):
+    """sum_g fxc_sf(g) (phi_o phi_v)(phi_o phi_v) over the grid (SF_TDA.py:509-556);
+    method 1: the multicollinear block of get_ab_sf (SF_TDA.py:1179-1272)."""
     if mf.xctype == 'HF':
         return 0.0
+    if method == 1:
+        from .mcol import sf_mc_block
+        return sf_mc_block(mf, mf.fxc_sf_mc, orbo, orbv)
     ao0 = mf.grids.ao[0]
     ro = ao0 @ orbo
     rv = ao0 @ orbv
@@ -124,7 +127,7 @@ def amat_down(mf, method=0):
     a = _exchange_block(mf, orbo_a, orbv_b, hyb) if (hyb != 0 or mf.omega != 0) else \
         np.zeros((nocc_a, nvir_b, nocc_a, nvir_b))
     if method != 2:
-        a = a + _sf_xc_kernel_block(mf, orbo_a, orbv_b)
+        a = a + _sf_xc_kernel_block(mf, orbo_a, orbv_b, method)
     fockA, fockB = mf.fock_mo()
     e = np.einsum
     iC, iO, iV = np.eye(nc), np.eye(no), np.eye(nv)
@@ -175,7 +178,7 @@ def amat_up(mf, method=0):
     a = _exchange_block(mf, orbo_b, orbv_a, hyb) if (hyb != 0 or mf.omega != 0) else \
         np.zeros((nc, nv, nc, nv))
     if method != 2:
-        a = a + _sf_xc_kernel_block(mf, orbo_b, orbv_a)
+        a = a + _sf_xc_kernel_block(mf, orbo_b, orbv_a, method)
     fockA, fockB = mf.fock_mo()
     d_ij = np.eye(nc + no)
     d_ab = np.eye(nv + no)

@@ -174,8 +174,6 @@ class XSFOracle:
                                hd[nc:, no:].reshape(-1), hd[nc:, :no].reshape(-1)])
         if self.re:
             hdiag = self.compress_removed_hdiag(hdiag)
-        if self.method == 1:
-            raise NotImplementedError("multicollinear kernel needs mcfun (out of scope)")
         vresp = engines.gen_response_sf(mf, method=self.method)
         if self.SA > 0:
             fockA_hf, fockB_hf = mf.fock_mo_hf()

@@ -37,6 +37,9 @@ int main() {
   expect_err(xt_create(&d, &h), "create XSF SA>0 with one open shell");
   d.kind = XT_KIND_XTDA; d.sa = 0; d.xctype = 17;
   expect_err(xt_create(&d, &h), "create bad xctype");
+  d.kind = XT_KIND_SF_DOWN; d.xctype = XT_XC_GGA; d.no = 2; d.nc = 3; d.sf_kernel = 5;
+  expect_err(xt_create(&d, &h), "create bad sf_kernel");
+  d.sf_kernel = XT_SF_ALDA0;
   // null-context calls of every setter / query
   double buf[8] = {0};
   expect_err(xt_set_orbitals(nullptr, buf, buf, XT_PTR_HOST), "set_orbitals null");
@@ -53,6 +56,12 @@ int main() {
              "dgemm_strided negative m");
   expect_err(xt_dgemm_strided(4, 4, 4, 1, 1, 1.0, buf, 2, 4, 0, 0, buf, 4, 1, 0, 0, 0.0, buf, 4, 0, nullptr),
              "dgemm_strided A without a unit stride");
+  expect_err(xt_dgemm_strided(4, 4, 4, 1, 1, 1.0, buf, 4, 1, 0, 0, buf, 4, 1, 0, 0, 0.0, buf, 3, 0, nullptr),
+             "dgemm_strided ldc < n");
+  expect_err(xt_dgemm_strided(4, 4, 4, 1, 1, 1.0, nullptr, 4, 1, 0, 0, buf, 4, 1, 0, 0, 0.0, buf, 4, 0, nullptr),
+             "dgemm_strided null A");
+  expect_err(xt_dgemm_strided(4, 4, 4, 2, 1, 1.0, buf, 4, 1, -16, 0, buf, 4, 1, 16, 0, 0.0, buf, 4, 0, nullptr),
+             "dgemm_strided negative stride");
   expect_err(xt_int2e_cart(-1, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr, 0, 0, 0.0, nullptr,
                            nullptr, 0.0, 0, nullptr, 0, nullptr), "int2e negative npair");
   expect_err(xt_int2e_cart(1, nullptr, nullptr, nullptr, 1, nullptr, nullptr, nullptr, 4, 0, 0.0, nullptr,

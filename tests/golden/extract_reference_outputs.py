@@ -11,8 +11,12 @@ Sources (PySCF 2.12.1 / libxc 7.0.0 runs recorded by the reference authors):
   nuclear repulsion, cond(S), per-atom pruned grid sizes, total grid count,
   converged SCF energy, final Roothaan orbital energies.
 * cell 2 -- XSF-TDA (ALDA0, SA=3, remove=True) 10 roots in eV.
+* cell 3 -- XSF-TDA with the multicollinear kernel (``method=1``, 60 collinear
+  samples; the BHandHLYP fit makes fglobal = 0) 10 roots in eV, and the printed
+  fglobal.
 * cell 5 / 6 -- the same molecule with UKS: SCF energy, USF-TDA (XSF_TDA on a
   UKS mf: SA=0, no OO compression) 10 roots in eV and the Delta<S^2> list.
+* cell 7 -- USF-TDA with the multicollinear kernel: 10 roots, Delta<S^2> list.
 * ``example/spin up.ipynb`` cell 1 -- H 0 0 0; F 0 0 1.0 A ROKS/BHandHLYP aufbau
   triplet SCF energy.
 * ``example/TDA.ipynb`` (PySCF 2.11.0 / libxc 7.0.0), B3LYP / cc-pVDZ,
@@ -78,6 +82,9 @@ def main():
     out["xsf_roks_alda0_fglobal"] = float(re.search(r"fglobal ([-\d.]+)", xsf).group(1))
     # the eigenvalue list is the bracket after the "Converged [True ...]" line
     out["xsf_roks_alda0_ev"] = _floats(xsf[xsf.index("]", xsf.index("Converged")) + 1:].split("]")[0])
+    mc = "\n".join(_outputs(cells[3]))
+    out["xsf_roks_mc_fglobal"] = float(re.search(r"fglobal ([-\d.]+)", mc).group(1))
+    out["xsf_roks_mc_ev"] = _floats(mc[mc.index("]", mc.index("Converged")) + 1:].split("]")[0])
     log5 = "\n".join(_outputs(cells[5]))
     out["uks_bhandhlyp_e_tot"] = float(_floats(_outputs(cells[5])[-1])[0])
     s2 = re.findall(r"multiplicity <S\^2> = ([\d.]+)", log5)
@@ -86,6 +93,10 @@ def main():
     out["usf_uks_alda0_ev"] = _floats(usf[usf.index("]", usf.index("Converged")) + 1:].split("]")[0])
     tail = _outputs(cells[6])[-1]
     out["usf_uks_alda0_delta_s2"] = _floats(tail[:tail.index("]")])
+    umc = "\n".join(_outputs(cells[7]))
+    out["usf_uks_mc_ev"] = _floats(umc[umc.index("]", umc.index("Converged")) + 1:].split("]")[0])
+    tail = _outputs(cells[7])[-1]
+    out["usf_uks_mc_delta_s2"] = _floats(tail[:tail.index("]")])
 
     nb2 = json.load(open(os.path.join(REF, "spin up.ipynb")))
     up = "\n".join(_outputs(nb2["cells"][1]))
@@ -126,6 +137,8 @@ def main():
     assert len(out["ch2o_roks_b3lyp_analyze"]) == 12
 
     assert len(out["xsf_roks_alda0_ev"]) == 10 and len(out["usf_uks_alda0_ev"]) == 10
+    assert len(out["xsf_roks_mc_ev"]) == 10 and len(out["usf_uks_mc_ev"]) == 10
+    assert len(out["usf_uks_mc_delta_s2"]) == 10
     assert len(out["hf_631g_grid_ang_F"]) == 75 and len(out["hf_631g_grid_ang_H"]) == 50
     json.dump(out, open(OUT, "w"), indent=1)
     print(json.dumps(out, indent=1))

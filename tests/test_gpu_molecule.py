@@ -48,6 +48,50 @@ def test_xsf_tda_kernel_matches_reference(torch, kind, key, jk_mode):
         assert np.abs(np.asarray(ds) - reference_outputs()["usf_uks_alda0_delta_s2"]).max() < 1e-4
 
 
+@pytest.mark.parametrize("jk_mode", ["DF", "ERI8"])
+@pytest.mark.parametrize("kind,key", [("ROKS", "xsf_roks_mc_ev"), ("UKS", "usf_uks_mc_ev")])
+def test_xsf_tda_multicollinear_matches_reference(torch, kind, key, jk_mode):
+    """XSF_TDA(mf, method=1).kernel(nstates=10): the multicollinear kernel (60 samples,
+    computed on the device) through the one-channel GGA response engine, device
+    Davidson, against the printed multicollinear roots (example/XSF_TDA.ipynb cells 3
+    and 7) and, for UKS, the printed Delta<S^2>."""
+    from xtddft_amd import XSF_TDA
+    mf = hf_meanfield(kind)
+    if jk_mode == "ERI8":
+        mf = as_device_eri8(mf)
+    x = XSF_TDA(mf, method=1)
+    e_ev, v = x.kernel(nstates=10)
+    assert np.all(x.converged)
+    assert x._op.sf_kernel == "mc"
+    ref = np.asarray(reference_outputs()[key])
+    err = np.abs(np.asarray(e_ev) - ref).max() / HA2EV_XSF
+    assert err < TOL_HA, (e_ev, ref)
+    if kind == "ROKS":
+        assert x.fglobal == reference_outputs()["xsf_roks_mc_fglobal"]
+    else:
+        ds, _ = x.analyse()
+        assert np.abs(np.asarray(ds) - reference_outputs()["usf_uks_mc_delta_s2"]).max() < 1e-4
+
+
+@pytest.mark.parametrize("isf", [-1, 1])
+@pytest.mark.parametrize("kind", ["ROKS", "UKS"])
+def test_sf_tda_multicollinear_matches_oracle(torch, isf, kind):
+    """SF_TDA(mf, isf, method=1) (Davidson, 50 collinear samples, SF_TDA.py:219) on the
+    HF molecule: device roots equal the eigenvalues of the oracle's explicit matrix with
+    the multicollinear block of get_ab_sf (SF_TDA.py:1179-1272) on the same kernel."""
+    import dataclasses
+    from xtddft_amd import SF_TDA
+    from xtddft_amd.mcol import sf_mc_kernel
+    mf = hf_meanfield(kind)
+    x = SF_TDA(mf, isf=isf, method=1)
+    e_ev, _ = x.kernel(nstates=5)
+    assert np.all(x.converged)
+    mfo = dataclasses.replace(mf, fxc_sf_mc=sf_mc_kernel(mf, 50))
+    a = osf.amat_down(mfo, method=1) if isf == -1 else osf.amat_up(mfo, method=1)
+    w = np.linalg.eigvalsh(0.5 * (a + a.T))[:5]
+    assert np.abs(np.asarray(e_ev) / HA2EV - w).max() < 1e-7
+
+
 def test_xtda_on_roks_molecule_matches_oracle(torch):
     """X-TDA (XTDA.py:746-829) on the converged ROKS HF molecule: device Davidson
     roots equal the oracle's explicit-A eigenvalues (no reference printout exists

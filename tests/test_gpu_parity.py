@@ -281,3 +281,41 @@ def test_apply_boundary_checks(hiplib):
     assert op.apply(z, out=out) is out
     assert rel(out.cpu().numpy(), op.apply(z.cpu().numpy())) < 1e-14
     op.close()
+
+
+# ---- multicollinear spin-flip kernel (method=1, SF_TDA.py:855-1047) ----------
+@pytest.mark.parametrize("kind", ["RO", "U"])
+@pytest.mark.parametrize("xct", ["GGA", "LDA", "MGGA"])
+@pytest.mark.parametrize("op_kind", ["SF_DOWN", "SF_UP", "XSF"])
+@pytest.mark.parametrize("nz", [1, 5, 13])
+def test_sf_multicollinear(dev, kind, xct, op_kind, nz):
+    """Device spin-flip response with the multicollinear kernel (the one-channel GGA /
+    MGGA point kernels, the LDA scalar path) against the oracle's AO route of
+    nr_uks_fxc_sf_tda_mc (SF_TDA.py:976-1047) on the same synthetic kernel."""
+    mf = make_mf(nao=26, nc=5, no=2, xctype=xct, kind=kind, hyb=0.5)
+    kw = {}
+    if op_kind == "XSF":
+        o = oxsf.XSFOracle(mf, method=1)
+        kw = dict(sa=o.SA, fglobal=0.4, foo=0.8, remove=o.re)
+        vind, hdiag = o.gen_tda_operation_sf(foo=0.8, fglobal=0.4)
+    else:
+        vind, hdiag = osf.gen_tda_operation_sf(mf, -1 if op_kind == "SF_DOWN" else 1, method=1)
+    z = make_trial_vectors(nz, hdiag.size)
+    op = dev(mf, op_kind, sf_kernel="mc", mc_kernel=mf.fxc_sf_mc, **kw)
+    if op_kind == "XSF":
+        op.set_oo_basis(o.vects)
+    assert rel(op.apply(z), vind(z)) < RTOL
+    if nz == 5 and op_kind == "SF_DOWN":   # the kernel changes the operator: ALDA0 differs
+        alda0 = dev(mf, op_kind)
+        assert rel(alda0.apply(z), vind(z)) > 1e-3
+
+
+@pytest.mark.parametrize("nc", [60, 140, 270])
+def test_sf_multicollinear_many_occupied(dev, nc):
+    """The one-channel GGA point kernel's other variants: O > 128 (one vector per
+    reduction, 4 register chunks) and O > 256 (the LDS block kernel)."""
+    mf = make_mf(nao=nc + 2 + 21, nc=nc, no=2, xctype="GGA", hyb=0.5, ngrid=1500)
+    vind, hdiag = osf.gen_tda_operation_sf(mf, -1, method=1)
+    z = make_trial_vectors(3, hdiag.size)
+    op = dev(mf, "SF_DOWN", sf_kernel="mc", mc_kernel=mf.fxc_sf_mc)
+    assert rel(op.apply(z), vind(z)) < RTOL

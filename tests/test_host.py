@@ -28,7 +28,7 @@ def test_library_builds_and_exports_every_header_symbol(hiplib):
     for s in syms:
         assert hasattr(hiplib, s), s
     from xtddft_amd._capi import ABI_VERSION
-    assert hiplib.xt_abi_version() == ABI_VERSION == 5
+    assert hiplib.xt_abi_version() == ABI_VERSION == 6
 
 
 def test_desc_layout_matches_c_header(tmp_path):
@@ -57,6 +57,9 @@ def test_create_rejects_bad_descriptor_without_gpu(hiplib):
         _capi.check(rc, "xt_create")
     d = _capi.XtDesc(kind=0, restricted=0, nao=10, nmo=10, nc=3, no=2, nv=5, si=1.0)  # XTDA needs ROKS
     assert hiplib.xt_create(ctypes.byref(d), ctypes.byref(h)) == -1
+    d = _capi.XtDesc(kind=2, restricted=1, nao=10, nmo=10, nc=3, no=2, nv=5, sf_kernel=7)  # no such kernel
+    assert hiplib.xt_create(ctypes.byref(d), ctypes.byref(h)) == -1
+    assert b"sf_kernel" in hiplib.xt_last_error()
     d = _capi.XtDesc(kind=4, restricted=1, nao=10, nmo=10, nc=3, no=1, nv=6, sa=3)   # 2S-1 = 0
     assert hiplib.xt_create(ctypes.byref(d), ctypes.byref(h)) == -1
     assert b"2S-1" in hiplib.xt_last_error()
@@ -176,3 +179,22 @@ def test_host_asan_build_of_the_c_abi():
     r = subprocess.run(["bash", "tools/asan_host.sh"], cwd=ROOT, capture_output=True, text=True, timeout=1800)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "asan driver: ok" in r.stdout
+
+
+def test_device_mf_shards_concatenate_to_the_unsharded_tensors():
+    """make_device_mf generates the DF factor and the grid in fixed blocks, each from its
+    own seed: the shards of 2 and 3 ranks concatenate to the 1-rank tensors exactly, so a
+    sharded bench run solves the same operator as N = 1 (torch CPU generator here; the
+    device generator has the same block structure)."""
+    import torch
+    from xtddft_amd.synthetic import make_device_mf
+    kw = dict(nao=20, nc=4, no=2, naux=150, ngrid=140000, torch_device="cpu", sf_mc=True)
+    full = make_device_mf(**kw)
+    for n in (2, 3):
+        parts = [make_device_mf(shard=(r, n), **kw) for r in range(n)]
+        assert torch.equal(torch.cat([p.grids.ao for p in parts], 1), full.grids.ao)
+        assert torch.equal(torch.cat([p.grids.weights for p in parts]), full.grids.weights)
+        assert torch.equal(torch.cat([p.cderi for p in parts], 0), full.cderi)
+        assert torch.equal(torch.cat([p.fxc for p in parts], -1), full.fxc)
+        assert torch.equal(torch.cat([p.fxc_sf_mc for p in parts], -1), full.fxc_sf_mc)
+        assert torch.equal(make_device_mf(shard=(1, n), full_aux=True, **kw).cderi, full.cderi)

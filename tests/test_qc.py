@@ -253,6 +253,78 @@ def test_usf_delta_s2_matches_reference():
     assert np.abs(np.asarray(ds) - ref).max() < 1e-5
 
 
+def _mc_kernel_oracle(mfd, samples, with_rho=False):
+    """The oracle's multicollinear kernel (oracle.mcol: mcfun eval_xc_eff_sf restated)
+    from the SCF densities on the grid; the collinear functional by autograd on torch
+    CPU tensors (all host threads)."""
+    import torch
+    from oracle import mcol
+    from oracle.engines import _eval_rho
+    from xtddft_amd.qc import xc as _xc
+    dm = mfd.make_rdm1()
+    rho = np.array([_eval_rho(mfd.grids.ao, dm[s], mfd.xctype) for s in range(2)])
+
+    def ev(r, d):
+        return tuple(None if x is None else x.numpy()
+                     for x in _xc.eval_xc_eff_torch(mfd.xc, torch.as_tensor(r), d))
+    k = mcol.cache_xc_kernel_sf_mc(ev, rho, samples)
+    return (k, rho) if with_rho else k
+
+
+@pytest.mark.parametrize("kind,key", [("ROKS", "xsf_roks_mc_ev"), ("UKS", "usf_uks_mc_ev")])
+def test_oracle_xsf_multicollinear_roots_match_reference(kind, key):
+    """XSF_TDA(mf, method=1) (ROKS: SA=3, remove, fglobal fitted to 4 (cx - 1/2)^2 = 0 for
+    BHandHLYP, XSF_TDA.py:1517-1518; UKS: SA=0) with 60 collinear samples: the oracle's
+    explicit operator against the reference's printed multicollinear roots
+    (example/XSF_TDA.ipynb cells 3 and 7) to 1e-6 Ha (observed <= 4e-8), and the
+    printed Delta<S^2> of the UKS run."""
+    import dataclasses
+    mfd = dataclasses.replace(hf_meanfield(kind))
+    mfd.fxc_sf_mc = _mc_kernel_oracle(mfd, 60)
+    fg = oxsf.default_fglobal(mfd, method=1)
+    if kind == "ROKS":
+        assert fg == reference_outputs()["xsf_roks_mc_fglobal"] == 0.0
+    o = oxsf.XSFOracle(mfd, method=1)
+    vind, hdiag = o.gen_tda_operation_sf(fglobal=fg)
+    a = vind(np.eye(hdiag.size)).T
+    w, v = np.linalg.eigh(0.5 * (a + a.T))
+    e = w[:10] * HA2EV_XSF
+    ref = np.asarray(reference_outputs()[key])
+    assert np.abs(e - ref).max() / HA2EV_XSF < 1e-6, e - ref
+    # the explicit matrix get_ab_sf (SF_TDA.py:1051-1276) is the same operator
+    if kind == "UKS":
+        from oracle.sf_tda import amat_down
+        assert np.abs(amat_down(mfd, method=1) - a).max() < 1e-12 * np.abs(a).max()
+        from xtddft_amd.xsf_tda import delta_s2_u
+        ds = [delta_s2_u(mfd, v[:, n], o.nc, o.no, o.nv) - o.no + 1 for n in range(10)]
+        assert np.abs(np.asarray(ds) - reference_outputs()["usf_uks_mc_delta_s2"]).max() < 1e-5
+
+
+@pytest.mark.parametrize("kind", ["ROKS", "UKS_TPSS"])
+def test_multicollinear_kernel_product_equals_oracle(kind):
+    """xtddft_amd.mcol.sf_mc_kernel (batched samples, torch) = the oracle's restatement of
+    mcfun's sampling (per-sample ud -> ts rotation), GGA and MGGA (tau_s row / column), on
+    the same ground-state densities (TPSS's z = tau_W / tau clamp makes its kernel jump
+    with the last bit of tau where one orbital dominates); the product's own densities
+    agree with the oracle's to round-off."""
+    import dataclasses
+    from xtddft_amd.mcol import ground_state_rho, sf_mc_kernel
+    import torch
+    mfd = dataclasses.replace(hf_meanfield(kind), extra=dict(hf_meanfield(kind).extra))
+    k_ref, rho = _mc_kernel_oracle(mfd, 8, with_rho=True)
+    rho_p = ground_state_rho(mfd, torch.device("cpu")).numpy()
+    assert np.abs(rho_p - rho).max() <= 1e-13 * np.abs(rho).max()
+    k = sf_mc_kernel(mfd, 8, max_points=40000, rho=rho)
+    nk = 5 if kind.endswith("TPSS") else 4
+    assert k.shape == (nk, nk, mfd.grids.ngrid)
+    # the (t, s) rotation 1/4 (f_aa - f_ab - f_ba + f_bb) cancels where one spin channel
+    # dominates; summed in a different order here and in the oracle (einsum): TPSS's
+    # kernel reaches 2e7 there, its round-off 2e-3
+    tol = 1e-9 if kind.endswith("TPSS") else 1e-12
+    assert np.abs(k - k_ref).max() <= tol * np.abs(k_ref).max()
+    assert np.abs(k - k.transpose(1, 0, 2)).max() == 0.0
+
+
 def test_chiral_mol():
     """gto.mole.chiral_mol (XTDA.py:818): mirror-image superposition test."""
     from xtddft_amd.qc.gto import chiral_mol

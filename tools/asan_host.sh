@@ -11,12 +11,15 @@ HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 FLAGS=(--offload-arch=gfx950 -O1 -g -fPIC -std=c++17 -Wno-unused-result
        -Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer)
 objs=()
+pids=()
+rm -f "$OUT"/*.o        # never link a stale object left by an earlier run
 for f in xtddft_amd/csrc/*.hip; do
   o="$OUT/$(basename "${f%.hip}").o"
   "$HIPCC" "${FLAGS[@]}" -c "$f" -o "$o" &
+  pids+=($!)
   objs+=("$o")
 done
-wait
+for p in "${pids[@]}"; do wait "$p" || { echo "asan compile failed"; exit 1; }; done
 echo 'const char* xt_build_id(void) { return "asan-host-build"; }' > "$OUT/xt_build_id.c"
 gcc -O1 -fPIC -c "$OUT/xt_build_id.c" -o "$OUT/xt_build_id.o"
 objs+=("$OUT/xt_build_id.o")

@@ -18,6 +18,7 @@ XT_PTR_DEVICE = 1
 KIND = {"XTDA": 0, "UTDA": 1, "SF_DOWN": 2, "SF_UP": 3, "XSF": 4}
 XC = {"HF": 0, "LDA": 1, "GGA": 2, "MGGA": 3}
 K_MODE = {"auto": 0, "direct": 1, "stored": 2}
+SF_KERNEL = {"alda0": 0, "mc": 1}
 K_MODE_NAME = {v: k for k, v in K_MODE.items()}
 
 ERRORS = {-1: ValueError, -2: MemoryError, -3: RuntimeError, -4: RuntimeError, -5: RuntimeError}
@@ -39,11 +40,11 @@ class XtDesc(ctypes.Structure):
         ("nc", c_int), ("no", c_int), ("nv", c_int), ("naux", c_int), ("ngrid", c_int),
         ("xctype", c_int), ("hyb", c_double), ("alpha", c_double), ("omega", c_double),
         ("si", c_double), ("sa", c_int), ("foo", c_double), ("fglobal", c_double),
-        ("remove", c_int), ("add_local", c_int), ("device", c_int),
+        ("remove", c_int), ("add_local", c_int), ("device", c_int), ("sf_kernel", c_int),
     ]
 
 
-ABI_VERSION = 5   # include/xtddft_amd.h XT_ABI_VERSION
+ABI_VERSION = 6   # include/xtddft_amd.h XT_ABI_VERSION
 
 
 class LibraryMissing(RuntimeError):

@@ -204,14 +204,17 @@ int xt_create(const xt_desc* desc, xt_ctx** out) {
   if (d.kind == XT_KIND_XSF && d.remove && d.no < 1)
     return fail(XT_ERR_ARG, "XSF OO compression needs an open shell");
   if (d.xctype < XT_XC_NONE || d.xctype > XT_XC_MGGA) return fail(XT_ERR_ARG, "bad xctype");
-  // (spin flip: ALDA0 uses densities only, the grid needs ao[0] only, SF_TDA.py:73-80)
+  const bool sf = (d.kind == XT_KIND_SF_DOWN || d.kind == XT_KIND_SF_UP || d.kind == XT_KIND_XSF);
+  if (sf && d.sf_kernel != XT_SF_ALDA0 && d.sf_kernel != XT_SF_MC) return fail(XT_ERR_ARG, "bad sf_kernel");
+  // spin flip: ALDA0 uses densities only, the grid needs ao[0] only (SF_TDA.py:73-80); the
+  // multicollinear kernel is GGA / MGGA-shaped over (s, grad s[, tau_s]) (SF_TDA.py:997-1041)
+  const bool dens_only = sf && d.sf_kernel == XT_SF_ALDA0;
   HIPCHK(hipSetDevice(d.device));
   xt_ctx* c = new xt_ctx();
   c->d = d;
   c->nbasis = d.restricted ? 1 : 2;
-  const bool sf = (d.kind == XT_KIND_SF_DOWN || d.kind == XT_KIND_SF_UP || d.kind == XT_KIND_XSF);
-  c->ncomp = ((d.xctype == XT_XC_GGA || d.xctype == XT_XC_MGGA) && !sf) ? 4 : 1;
-  c->nkc = (d.xctype == XT_XC_MGGA && !sf) ? 5 : c->ncomp;
+  c->ncomp = ((d.xctype == XT_XC_GGA || d.xctype == XT_XC_MGGA) && !dens_only) ? 4 : 1;
+  c->nkc = (d.xctype == XT_XC_MGGA && !dens_only) ? 5 : c->ncomp;
   const int nb = d.restricted ? 0 : 1;   // beta basis index
   if (d.kind == XT_KIND_XTDA || d.kind == XT_KIND_UTDA) {
     c->nchan = 2; c->O = d.nc + d.no; c->V = d.no + d.nv; c->v0 = d.nc;
@@ -489,7 +492,7 @@ int xt_set_grid(xt_ctx* c, const double* ao, const double* w, const double* kern
   (void)hipSetDevice(c->d.device);
   const int nao = c->d.nao, nmo = c->d.nmo, ng = c->d.ngrid;
   const bool sf = (c->d.kind == XT_KIND_SF_DOWN || c->d.kind == XT_KIND_SF_UP || c->d.kind == XT_KIND_XSF);
-  // input ao carries ncomp_in components (4 for GGA even on the SF path, which only uses ao[0])
+  // input ao carries c->ncomp components (1 for the density-only ALDA0 spin-flip kernel)
   const int ncomp = c->ncomp;
   // + zeroed slack rows after the last plane (fused XC kernels read whole K-tiles)
   const size_t phi_used = (size_t)c->nbasis * ncomp * ng * nmo;
@@ -516,15 +519,16 @@ int xt_set_grid(xt_ctx* c, const double* ao, const double* w, const double* kern
       }
     }
   }
-  if (sf) {
+  if (sf && c->d.sf_kernel == XT_SF_ALDA0) {
     RET(to_device(c, c->kern, kernel, (size_t)ng, ptr_kind));   // already weighted
   } else {
-    const size_t n4 = (size_t)4 * c->nkc * c->nkc;
+    // UKS fxc (2, nk, 2, nk) x w, or the multicollinear spin-flip kernel (nk, nk) x 2 w
+    const size_t n4 = (size_t)(sf ? 1 : 4) * c->nkc * c->nkc;
     RET(to_device(c, c->kern, kernel, n4 * ng, ptr_kind));
     RET(c->stage2.ensure(ng));
     const hipMemcpyKind k = ptr_kind == XT_PTR_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
     HIPCHK(hipMemcpyAsync(c->stage2.p, w, (size_t)ng * 8, k, c->st));
-    weight_fxc(c->st, (long)n4, ng, c->stage2.p, c->kern.p);
+    weight_fxc(c->st, (long)n4, ng, sf ? 2.0 : 1.0, c->stage2.p, c->kern.p);
   }
   HIPCHK(hipStreamSynchronize(c->st));
   c->stage.release(); c->stage2.release();
@@ -843,6 +847,7 @@ static int build_kx(xt_ctx* c) {
       }
     }
     kx_mirror(c->st, O, V, (long)ld, i0, i1, KX_FOLD, K);
+    HIPCHK(hipGetLastError());   // a rejected mirror launch would leave zero blocks in Kx
   }
   HIPCHK(hipStreamSynchronize(c->st));
   c->kx_valid = true;
@@ -1068,15 +1073,21 @@ static int xc_response(xt_ctx* c, int nz) {
       if (mgga) {
         double* Ts[2];
         for (int s = 0; s < 2; ++s) Ts[s] = c->taubuf.p + (Us[s] - c->ubuf.p);   // same layout as U
-        xc_uks_mgga(c->st, n, g0, ng, nz, O, nmo, compP, c->Phi.p + c->occ_basis[0] * basP,
+        xc_uks_mgga(c->st, 2, n, g0, ng, nz, O, nmo, compP, c->Phi.p + c->occ_basis[0] * basP,
                     c->Phi.p + c->occ_basis[1] * basP, c->kern.p, Us[0], lus[0], Us[1], lus[1], Ts[0], Ts[1],
                     (long)nch * nz * O * n, Rs[0], lrs[0], Rs[1], lrs[1]);
       } else {
-        xc_uks_w(c->st, nc, n, g0, ng, nz, O, nmo, compP,
+        xc_uks_w(c->st, 2, nc, n, g0, ng, nz, O, nmo, compP,
                  c->Phi.p + c->occ_basis[0] * basP, c->Phi.p + c->occ_basis[1] * basP,
                  c->kern.p, Us[0], lus[0], Us[1], lus[1], Rs[0], lrs[0], Rs[1], lrs[1]);
       }
-    } else {
+    } else if (mgga) {   // one spin-flip channel, multicollinear (rho, grad rho, tau) kernel
+      xc_uks_mgga(c->st, 1, n, g0, ng, nz, O, nmo, compP, c->Phi.p + c->occ_basis[0] * basP, nullptr, c->kern.p,
+                  Ug[0], ldU[0], nullptr, 0, c->taubuf.p, nullptr, (long)nz * O * n, Rg[0], ldR[0], nullptr, 0);
+    } else if (gga) {    // one spin-flip channel, multicollinear (rho, grad rho) kernel
+      xc_uks_w(c->st, 1, nc, n, g0, ng, nz, O, nmo, compP, c->Phi.p + c->occ_basis[0] * basP, nullptr, c->kern.p,
+               Ug[0], ldU[0], nullptr, 0, Rg[0], ldR[0], nullptr, 0);
+    } else {             // ALDA0, or the multicollinear LDA kernel (2 w f_ss: scalar)
       xc_sf(c->st, n, g0, nz, O, nmo, c->Phi.p + c->occ_basis[0] * basP, c->kern.p, Ug[0]);
     }
     for (int q = 0; q < ngr; ++q) {
@@ -1420,6 +1431,11 @@ extern "C" int xt_dgemm_strided(int m, int n, int k, int r, int nbatch, double a
   if (m < 0 || n < 0 || k < 0 || r < 1 || nbatch < 1) return fail(XT_ERR_ARG, "xt_dgemm_strided: bad sizes");
   if (sAm != 1 && sAk != 1) return fail(XT_ERR_ARG, "xt_dgemm_strided: A needs a unit m or k stride");
   if (sBn != 1 && sBk != 1) return fail(XT_ERR_ARG, "xt_dgemm_strided: B needs a unit k or n stride");
+  if (sAm < 0 || sAk < 0 || sAr < 0 || sAb < 0 || sBk < 0 || sBn < 0 || sBr < 0 || sBb < 0 || sCb < 0)
+    return fail(XT_ERR_ARG, "xt_dgemm_strided: negative stride");
+  if (ldc < n) return fail(XT_ERR_ARG, "xt_dgemm_strided: ldc < n");
+  if ((long)m * n > 0 && (!cc || (k > 0 && (!a || !b))))
+    return fail(XT_ERR_ARG, "xt_dgemm_strided: null operand");
   GemmDesc g;
   g.M = m; g.N = n; g.K = k; g.R = r; g.nb1 = nbatch;
   g.A = a; g.sAm = sAm; g.sAk = sAk; g.sAr = sAr; g.sAb1 = sAb;

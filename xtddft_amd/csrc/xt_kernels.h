@@ -14,15 +14,17 @@ void xsf_rank1(hipStream_t st, int nz, int nc, int no, int nv, int nmo, double a
 void ediag(hipStream_t st, int nz, int O, int V, int nmo, int v0, const double* eps, const double* ze, double* acc);
 void xc_uks(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, int nmo,
             const double* phi0, const double* phi1, const double* wfxc, double* U);
-void xc_uks_w(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
+// ns = 2: both spin channels of the UKS response (kernel (2, nk, 2, nk, ngrid)); ns = 1: one
+// spin-flip channel with the multicollinear kernel (nk, nk, ngrid); U1 / R1 / pO1 unused
+void xc_uks_w(hipStream_t st, int ns, int ncomp, int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
               const double* pO0, const double* pO1, const double* wfxc, double* U0, long ldU0,
               double* U1, long ldU1, double* R0, long ldR0, double* R1, long ldR1);
 void xc_sf(hipStream_t st, int G, int g0, int nz, int O, int nmo, const double* phio, const double* fsf, double* U);
-void weight_fxc(hipStream_t st, long n4, int ngrid, const double* w, double* f);
+void weight_fxc(hipStream_t st, long n4, int ngrid, double scale, const double* w, double* f);
 // meta-GGA point kernel: GGA terms + tau (T_s[c] planes tcs apart, same leading dims as U)
-void xc_uks_mgga(hipStream_t st, int G, int g0, int ngrid, int nz, int O, int nmo, long compP, const double* pO0,
-                 const double* pO1, const double* wfxc, double* U0, long ldU0, double* U1, long ldU1, double* T0,
-                 double* T1, long tcs, double* R0, long ldR0, double* R1, long ldR1);
+void xc_uks_mgga(hipStream_t st, int ns, int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
+                 const double* pO0, const double* pO1, const double* wfxc, double* U0, long ldU0, double* U1,
+                 long ldU1, double* T0, double* T1, long tcs, double* R0, long ldR0, double* R1, long ldR1);
 void xsf_assemble(hipStream_t st, int nz, int nc, int no, int nv, int remove, const double* vects, const double* z, double* ze);
 // XSF exchange through the stored matrix: the trial vectors split into their four
 // spin-adaptation source blocks (cv, co, ov, oo), and the per-block results combined

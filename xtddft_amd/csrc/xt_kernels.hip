@@ -276,7 +276,10 @@ k_xc_uks(int G, int g0, int ngrid, int nz, int O, int nmo,
 // inside the back GEMM.  The grid point's occupied MO values / gradients and
 // the 2NC x 2NC kernel block are staged once in LDS and reused by all 2*nz
 // vectors; each wave handles one x for both spins (HBM-bound on U / L).
-template <int NC>
+// NS = 2: the spin-conserving UKS response (nr_uks_fxc); NS = 1: one spin-flip channel
+// with the multicollinear kernel (nr_uks_fxc_sf_tda_mc, SF_TDA.py:976-1047), kernel
+// layout (NC, NC, ngrid) -- the same contraction with the spin index dropped.
+template <int NC, int NS>
 __global__ void __launch_bounds__(256, 4)
 k_xc_uks_w(int g0, int ngrid, int nz, int O, int nmo, long compP,
            const double* __restrict__ pO0, const double* __restrict__ pO1,
@@ -284,10 +287,10 @@ k_xc_uks_w(int g0, int ngrid, int nz, int O, int nmo, long compP,
            double* __restrict__ U0, long ldU0, double* __restrict__ U1, long ldU1,
            double* __restrict__ R0, long ldR0, double* __restrict__ R1, long ldR1) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  __shared__ double sk[4 * NC * NC];   // sk[((t*NC + y')*2 + s)*NC + y] = (w fxc) at this point
+  __shared__ double sk[NS * NS * NC * NC];   // sk[((t*NC + y')*NS + s)*NC + y] = (w fxc) at this point
   const int g = blockIdx.x;
   const long gg = g0 + g;
-  const bool same = (pO0 == pO1);
+  const bool same = (NS == 1 || pO0 == pO1);
   const double* so[2];
   so[0] = sm;
   so[1] = same ? so[0] : sm + NC * O;
@@ -299,31 +302,29 @@ k_xc_uks_w(int g0, int ngrid, int nz, int O, int nmo, long compP,
       dso[k] = po[cc * compP + gg * nmo + i];
     }
   }
-  for (int k = threadIdx.x; k < 4 * NC * NC; k += blockDim.x) sk[k] = wfxc[(long)k * ngrid + gg];
+  for (int k = threadIdx.x; k < NS * NS * NC * NC; k += blockDim.x) sk[k] = wfxc[(long)k * ngrid + gg];
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nwave = blockDim.x >> 6;
   double* Ub[2] = {U0 + g * ldU0, U1 + g * ldU1};
   double* Rb[2] = {R0 ? R0 + g * ldR0 : nullptr, R1 ? R1 + g * ldR1 : nullptr};
   for (int x = wave; x < nz; x += nwave) {
-    double acc[2][NC];
+    double acc[NS][NC];
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < NS; ++s)
 #pragma unroll
       for (int c = 0; c < NC; ++c) acc[s][c] = 0.0;
-    const double* u0 = Ub[0] + (long)x * O;
-    const double* u1 = Ub[1] + (long)x * O;
     for (int i = lane; i < O; i += 64) {
-      const double a0 = u0[i], a1 = u1[i];
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        acc[0][c] += a0 * so[0][c * O + i];
-        acc[1][c] += a1 * so[1][c * O + i];
+      for (int s = 0; s < NS; ++s) {
+        const double a = Ub[s][(long)x * O + i];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[s][c] += a * so[s][c * O + i];
       }
     }
-    double rho[2][NC];
+    double rho[NS][NC];
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < NS; ++s)
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         double v = acc[s][c];
@@ -332,23 +333,23 @@ k_xc_uks_w(int g0, int ngrid, int nz, int O, int nmo, long compP,
         if (NC > 1 && c > 0) v += Rb[s][3 * x + c - 1];
         rho[s][c] = v;
       }
-    double wv[2][NC];
-    // keep the 4 NC^2 kernel values in LDS (re-read per x): hoisted out of the
-    // x loop they would pin 2*4 NC^2 VGPRs
+    double wv[NS][NC];
+    // keep the NS^2 NC^2 kernel values in LDS (re-read per x): hoisted out of the
+    // x loop they would pin 2 NS^2 NC^2 VGPRs
     asm volatile("" ::: "memory");
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < NS; ++s)
 #pragma unroll
       for (int y = 0; y < NC; ++y) {
         double v = 0.0;
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < NS; ++t)
 #pragma unroll
-          for (int yy = 0; yy < NC; ++yy) v += sk[((t * NC + yy) * 2 + s) * NC + y] * rho[t][yy];
+          for (int yy = 0; yy < NC; ++yy) v += sk[((t * NC + yy) * NS + s) * NC + y] * rho[t][yy];
         wv[s][y] = v;
       }
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NS; ++s) {
       double* u = Ub[s] + (long)x * O;
       for (int i = lane; i < O; i += 64) {
         double l = 0.0;
@@ -357,11 +358,11 @@ k_xc_uks_w(int g0, int ngrid, int nz, int O, int nmo, long compP,
         u[i] = l;
       }
     }
-    if (NC > 1 && lane < 6) {   // all reads of R for this x are done (shuffle-synchronised wave)
+    if (NC > 1 && lane < 3 * NS) {   // all reads of R for this x are done (shuffle-synchronised wave)
       const int s = lane / 3, c = lane % 3 + 1;
       double v = 0.0;
 #pragma unroll
-      for (int ss = 0; ss < 2; ++ss)
+      for (int ss = 0; ss < NS; ++ss)
 #pragma unroll
         for (int y = 1; y < NC; ++y)
           if (ss == s && y == c) v = wv[ss][y];
@@ -431,22 +432,22 @@ __device__ __forceinline__ double wave_sum_transpose(double (&v)[NV], int lane) 
   return t;
 }
 
-template <int NC, int IC>
+template <int NC, int IC, int NS>
 __global__ void __launch_bounds__(256)
 k_xc_point(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
            const double* __restrict__ pO0, const double* __restrict__ pO1,
            const double* __restrict__ wfxc,
            double* __restrict__ U0, long ldU0, double* __restrict__ U1, long ldU1,
            double* __restrict__ R0, long ldR0, double* __restrict__ R1, long ldR1) {
-  constexpr int NV = 2 * NC;
-  constexpr int SH = NV == 8 ? 3 : (NV == 2 ? 5 : 4);   // value j lives at lanes j << SH
+  constexpr int NV = NS * NC;
+  constexpr int SH = NV == 8 ? 3 : (NV == 4 ? 4 : (NV == 2 ? 5 : 6));   // value j lives at lanes j << SH
   const int lane = threadIdx.x & 63;
   const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (g >= G) return;   // whole waves only; no block-level synchronisation below
   const long gg = g0 + g;
-  double ph[2][NC][IC];
+  double ph[NS][NC][IC];
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < NS; ++s) {
     const double* po = s ? pO1 : pO0;
 #pragma unroll
     for (int c = 0; c < NC; ++c)
@@ -462,16 +463,16 @@ k_xc_point(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int t = k / NC, yy = k % NC;
-    fk[k] = lane < NV ? wfxc[(long)(((t * NC + yy) * 2 + sl) * NC + yl) * ngrid + gg] : 0.0;
+    fk[k] = lane < NV ? wfxc[(long)(((t * NC + yy) * NS + sl) * NC + yl) * ngrid + gg] : 0.0;
   }
   double* Ub[2] = {U0 + g * ldU0, U1 + g * ldU1};
   double* Rb[2] = {R0 ? R0 + g * ldR0 : nullptr, R1 ? R1 + g * ldR1 : nullptr};
   // the next x's U row and rhoW values are loaded before this x's reductions, so
   // two rows per wave are in flight (the loop is HBM-latency-bound otherwise)
-  double un[2][IC], rn[2][NC > 1 ? NC - 1 : 1];
+  double un[NS][IC], rn[NS][NC > 1 ? NC - 1 : 1];
   auto load_x = [&](int x) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NS; ++s) {
 #pragma unroll
       for (int m = 0; m < IC; ++m) {
         const int i = lane + 64 * m;
@@ -485,9 +486,9 @@ k_xc_point(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
   };
   load_x(0);
   for (int x = 0; x < nz; ++x) {
-    double u[2][IC], rw_[2][NC > 1 ? NC - 1 : 1];
+    double u[NS][IC], rw_[NS][NC > 1 ? NC - 1 : 1];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NS; ++s) {
 #pragma unroll
       for (int m = 0; m < IC; ++m) u[s][m] = un[s][m];
 #pragma unroll
@@ -496,7 +497,7 @@ k_xc_point(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
     if (x + 1 < nz) load_x(x + 1);
     double v[NV];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NS; ++s) {
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         double a = 0.0;
@@ -511,7 +512,7 @@ k_xc_point(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
     for (int j = 0; j < NV; ++j) rho[j] = readlane_d(tot, j << SH);
     if constexpr (NC > 1) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int c = 1; c < NC; ++c) rho[s * NC + c] += rw_[s][c - 1];
     }
@@ -522,7 +523,7 @@ k_xc_point(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
 #pragma unroll
     for (int j = 0; j < NV; ++j) wv[j] = readlane_d(wl, j);
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < NS; ++s)
 #pragma unroll
       for (int m = 0; m < IC; ++m) {
         const int i = lane + 64 * m;
@@ -584,14 +585,14 @@ __device__ __forceinline__ double wave_sum_transpose32(double (&v)[32], int lane
 // vector, the NV rho of that vector gathered through 256 B of LDS), and the wv values go back
 // to the occupied lanes through LDS broadcast reads.  Same arithmetic per (point, vector).
 // The next batch's U rows are loaded while this one is reduced.
-template <int NC, int IC>
+template <int NC, int IC, int NS>
 __global__ void __launch_bounds__(256)
 k_xc_point_b(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
              const double* __restrict__ pO0, const double* __restrict__ pO1,
              const double* __restrict__ wfxc,
              double* __restrict__ U0, long ldU0, double* __restrict__ U1, long ldU1,
              double* __restrict__ R0, long ldR0, double* __restrict__ R1, long ldR1) {
-  constexpr int NV = 2 * NC, XB = 32 / NV;
+  constexpr int NV = NS * NC, XB = 32 / NV;
   __shared__ __attribute__((aligned(16))) double sh[4][2][32];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = blockIdx.x * 4 + wid;
@@ -599,9 +600,9 @@ k_xc_point_b(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
   const long gg = g0 + g;
   double* rs = sh[wid][0];
   double* ws = sh[wid][1];
-  double ph[2][NC][IC];
+  double ph[NS][NC][IC];
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < NS; ++s) {
     const double* po = s ? pO1 : pO0;
 #pragma unroll
     for (int c = 0; c < NC; ++c)
@@ -617,31 +618,31 @@ k_xc_point_b(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int t = k / NC, yy = k % NC;
-    fk[k] = wfxc[(long)(((t * NC + yy) * 2 + sl) * NC + yl) * ngrid + gg];
+    fk[k] = wfxc[(long)(((t * NC + yy) * NS + sl) * NC + yl) * ngrid + gg];
   }
   double* Ub[2] = {U0 + g * ldU0, U1 + g * ldU1};
   double* Rl = (NC > 1 && yl > 0) ? (sl ? R1 + g * ldR1 : R0 + g * ldR0) + yl - 1 : nullptr;
   // batch loads: U rows of XB vectors (lanes over occupied), this lane's rhoW value.
   // Branch-free: lanes past O and vectors past nz read a clamped (valid) element and
   // keep zero.
-  const double* ul[2][IC];
+  const double* ul[NS][IC];
   bool iv[IC];
 #pragma unroll
   for (int m = 0; m < IC; ++m) {
     const int i = lane + 64 * m;
     iv[m] = i < O;
-    ul[0][m] = Ub[0] + (i < O ? i : O - 1);
-    ul[1][m] = Ub[1] + (i < O ? i : O - 1);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) ul[s][m] = Ub[s] + (i < O ? i : O - 1);
   }
   const double* rl = Rl ? Rl : (R0 ? R0 + g * ldR0 : Ub[0]);
-  double un[XB][2][IC], rn;
-  auto load_b = [&](int x0, double (&ub)[XB][2][IC], double& rb) __attribute__((always_inline)) {
+  double un[XB][NS][IC], rn;
+  auto load_b = [&](int x0, double (&ub)[XB][NS][IC], double& rb) __attribute__((always_inline)) {
 #pragma unroll
     for (int xb = 0; xb < XB; ++xb) {
       const int x = x0 + xb < nz ? x0 + xb : nz - 1;
       const bool xv = x0 + xb < nz;
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int m = 0; m < IC; ++m) {
           const double t = ul[s][m][(long)x * O];
@@ -655,12 +656,12 @@ k_xc_point_b(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
       rb = (Rl && x0 + xbl < nz) ? t : 0.0;
     }
   };
-  auto body = [&](int x0, const double (&u)[XB][2][IC], double r) __attribute__((always_inline)) {
+  auto body = [&](int x0, const double (&u)[XB][NS][IC], double r) __attribute__((always_inline)) {
     double v[32];
 #pragma unroll
     for (int xb = 0; xb < XB; ++xb)
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
           double a = 0.0;
@@ -693,7 +694,7 @@ k_xc_point_b(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
       }
       if (x0 + xb < nz) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+        for (int s = 0; s < NS; ++s)
 #pragma unroll
           for (int m = 0; m < IC; ++m) {
             const int i = lane + 64 * m;
@@ -709,11 +710,11 @@ k_xc_point_b(int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
   };
   load_b(0, un, rn);
   for (int x0 = 0; x0 < nz; x0 += XB) {
-    double u[XB][2][IC];
+    double u[XB][NS][IC];
 #pragma unroll
     for (int xb = 0; xb < XB; ++xb)
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int m = 0; m < IC; ++m) u[xb][s][m] = un[xb][s][m];
     const double r = rn;
@@ -798,9 +799,10 @@ k_xc_sf_pt(int G, int g0, int nz, int O, int nmo, const double* __restrict__ phi
   }
 }
 
-// wfxc = fxc * w  (fxc layout (2,nc,2,nc,ngrid))
-__global__ void k_weight_fxc(long n4, int ngrid, const double* __restrict__ w, double* __restrict__ f) {
-  GRID_STRIDE(t, n4 * ngrid) f[t] *= w[t % ngrid];
+// wfxc = scale * fxc * w  (fxc layout (2,nc,2,nc,ngrid), or (nc,nc,ngrid) with scale 2 for the
+// multicollinear spin-flip kernel: wv = einsum('bg,abg->ag', rho1sf, 2 fxc) w, SF_TDA.py:1003)
+__global__ void k_weight_fxc(long n4, int ngrid, double scale, const double* __restrict__ w, double* __restrict__ f) {
+  GRID_STRIDE(t, n4 * ngrid) f[t] *= scale * w[t % ngrid];
 }
 
 // ---- XSF: cv|co|ov|oo blocks <-> full (nocc_a x nvir_b) spin-flip block ----
@@ -1030,7 +1032,10 @@ void xc_uks(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, 
 // the 5 x 5 (rho, grad rho, tau) kernel block, and the tau potential's back operands
 //   T_s[c][x][i] <- 1/2 wv[s][4] dPhiO_c[i]       (sigma += T_c^T dPhiV_c, GEMMs).
 // One block per grid point, one wave per trial vector x (both spins); correctness
-// first (the MGGA classes are plain GEMMs around it).
+// first (the MGGA classes are plain GEMMs around it).  NS = 1: one spin-flip channel
+// with the multicollinear (rho, grad rho, tau) kernel (nr_uks_fxc_sf_tda_mc's MGGA branch,
+// SF_TDA.py:1028-1041), kernel layout (NK, NK, ngrid).
+template <int NS>
 __global__ void __launch_bounds__(256)
 k_xc_uks_mgga(int g0, int ngrid, int nz, int O, int nmo, long compP,
               const double* __restrict__ pO0, const double* __restrict__ pO1,
@@ -1040,10 +1045,10 @@ k_xc_uks_mgga(int g0, int ngrid, int nz, int O, int nmo, long compP,
               double* __restrict__ R0, long ldR0, double* __restrict__ R1, long ldR1) {
   constexpr int NC = 4, NK = 5;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  __shared__ double sk[4 * NK * NK];   // sk[((t*NK + y')*2 + s)*NK + y] = (w fxc) at this point
+  __shared__ double sk[NS * NS * NK * NK];   // sk[((t*NK + y')*NS + s)*NK + y] = (w fxc) at this point
   const int g = blockIdx.x;
   const long gg = g0 + g;
-  const bool same = (pO0 == pO1);
+  const bool same = (NS == 1 || pO0 == pO1);
   const double* so[2];
   so[0] = sm;
   so[1] = same ? so[0] : sm + NC * O;
@@ -1055,7 +1060,7 @@ k_xc_uks_mgga(int g0, int ngrid, int nz, int O, int nmo, long compP,
       dso[k] = po[cc * compP + gg * nmo + i];
     }
   }
-  for (int k = threadIdx.x; k < 4 * NK * NK; k += blockDim.x) sk[k] = wfxc[(long)k * ngrid + gg];
+  for (int k = threadIdx.x; k < NS * NS * NK * NK; k += blockDim.x) sk[k] = wfxc[(long)k * ngrid + gg];
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nwave = blockDim.x >> 6;
@@ -1063,14 +1068,14 @@ k_xc_uks_mgga(int g0, int ngrid, int nz, int O, int nmo, long compP,
   double* Tb[2] = {T0 + g * ldU0, T1 + g * ldU1};
   double* Rb[2] = {R0 + g * ldR0, R1 + g * ldR1};
   for (int x = wave; x < nz; x += nwave) {
-    double acc[2][NK];
+    double acc[NS][NK];
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < NS; ++s)
 #pragma unroll
       for (int c = 0; c < NK; ++c) acc[s][c] = 0.0;
     for (int i = lane; i < O; i += 64) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < NS; ++s) {
         const double u = Ub[s][(long)x * O + i];
 #pragma unroll
         for (int c = 0; c < NC; ++c) acc[s][c] += u * so[s][c * O + i];
@@ -1078,9 +1083,9 @@ k_xc_uks_mgga(int g0, int ngrid, int nz, int O, int nmo, long compP,
         for (int c = 1; c < NC; ++c) acc[s][4] += Tb[s][(c - 1) * tcs + (long)x * O + i] * so[s][c * O + i];
       }
     }
-    double rho[2][NK];
+    double rho[NS][NK];
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < NS; ++s)
 #pragma unroll
       for (int c = 0; c < NK; ++c) {
         double v = acc[s][c];
@@ -1089,21 +1094,21 @@ k_xc_uks_mgga(int g0, int ngrid, int nz, int O, int nmo, long compP,
         if (c >= 1 && c <= 3) v += Rb[s][3 * x + c - 1];
         rho[s][c] = c == 4 ? 0.5 * v : v;
       }
-    double wv[2][NK];
+    double wv[NS][NK];
     asm volatile("" ::: "memory");
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < NS; ++s)
 #pragma unroll
       for (int y = 0; y < NK; ++y) {
         double v = 0.0;
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < NS; ++t)
 #pragma unroll
-          for (int yy = 0; yy < NK; ++yy) v += sk[((t * NK + yy) * 2 + s) * NK + y] * rho[t][yy];
+          for (int yy = 0; yy < NK; ++yy) v += sk[((t * NK + yy) * NS + s) * NK + y] * rho[t][yy];
         wv[s][y] = v;
       }
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NS; ++s) {
       for (int i = lane; i < O; i += 64) {
         double l = 0.0;
 #pragma unroll
@@ -1113,11 +1118,11 @@ k_xc_uks_mgga(int g0, int ngrid, int nz, int O, int nmo, long compP,
         for (int c = 1; c < NC; ++c) Tb[s][(c - 1) * tcs + (long)x * O + i] = 0.5 * wv[s][4] * so[s][c * O + i];
       }
     }
-    if (lane < 6) {   // all reads of R for this x are done (shuffle-synchronised wave)
+    if (lane < 3 * NS) {   // all reads of R for this x are done (shuffle-synchronised wave)
       const int s = lane / 3, c = lane % 3 + 1;
       double v = 0.0;
 #pragma unroll
-      for (int ss = 0; ss < 2; ++ss)
+      for (int ss = 0; ss < NS; ++ss)
 #pragma unroll
         for (int y = 1; y < NC; ++y)
           if (ss == s && y == c) v = wv[ss][y];
@@ -1125,44 +1130,56 @@ k_xc_uks_mgga(int g0, int ngrid, int nz, int O, int nmo, long compP,
     }
   }
 }
-void xc_uks_mgga(hipStream_t st, int G, int g0, int ngrid, int nz, int O, int nmo, long compP, const double* pO0,
-                 const double* pO1, const double* wfxc, double* U0, long ldU0, double* U1, long ldU1, double* T0,
-                 double* T1, long tcs, double* R0, long ldR0, double* R1, long ldR1) {
-  const bool same = (pO0 == pO1);
+void xc_uks_mgga(hipStream_t st, int ns, int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
+                 const double* pO0, const double* pO1, const double* wfxc, double* U0, long ldU0, double* U1,
+                 long ldU1, double* T0, double* T1, long tcs, double* R0, long ldR0, double* R1, long ldR1) {
+  if (G <= 0 || nz <= 0 || O <= 0) return;
+  const bool same = (ns == 1 || pO0 == pO1);
   const size_t lds = (same ? 1 : 2) * (size_t)4 * O * sizeof(double);
-  hipLaunchKernelGGL(k_xc_uks_mgga, dim3(G), dim3(256), lds, st, g0, ngrid, nz, O, nmo, compP, pO0, pO1, wfxc, U0,
-                     ldU0, U1, ldU1, T0, T1, tcs, R0, ldR0, R1, ldR1);
+  if (ns == 1)
+    hipLaunchKernelGGL(k_xc_uks_mgga<1>, dim3(G), dim3(256), lds, st, g0, ngrid, nz, O, nmo, compP, pO0, pO0, wfxc,
+                       U0, ldU0, U0, ldU0, T0, T0, tcs, R0, ldR0, R0, ldR0);
+  else
+    hipLaunchKernelGGL(k_xc_uks_mgga<2>, dim3(G), dim3(256), lds, st, g0, ngrid, nz, O, nmo, compP, pO0, pO1, wfxc,
+                       U0, ldU0, U1, ldU1, T0, T1, tcs, R0, ldR0, R1, ldR1);
 }
-void xc_uks_w(hipStream_t st, int ncomp, int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
+void xc_uks_w(hipStream_t st, int ns, int ncomp, int G, int g0, int ngrid, int nz, int O, int nmo, long compP,
               const double* pO0, const double* pO1, const double* wfxc, double* U0, long ldU0,
               double* U1, long ldU1, double* R0, long ldR0, double* R1, long ldR1) {
   if (G <= 0 || nz <= 0 || O <= 0) return;
+  if (ns == 1) {   // one spin-flip channel: the second channel's pointers are never read
+    pO1 = pO0; U1 = U0; ldU1 = ldU0; R1 = R0; ldR1 = ldR0;
+  }
   if (O <= 256) {   // one wave per grid point, occupied values in registers
     const dim3 grid((G + 3) / 4), blk(256);
-#define XT_POINT(NC, IC) hipLaunchKernelGGL((k_xc_point<NC, IC>), grid, blk, 0, st, G, g0, ngrid, nz, O, nmo, compP, \
-                                            pO0, pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1)
+#define XT_POINT(NC, IC, NS) hipLaunchKernelGGL((k_xc_point<NC, IC, NS>), grid, blk, 0, st, G, g0, ngrid, nz, O, nmo, \
+                                                compP, pO0, pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1)
+#define XT_POINT_B(IC, NS) hipLaunchKernelGGL((k_xc_point_b<4, IC, NS>), grid, blk, 0, st, G, g0, ngrid, nz, O, nmo, \
+                                              compP, pO0, pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1)
     // GGA, O <= 128: several vectors per reduction (k_xc_point_b; same box: C5 18.5-18.6 ->
     // 17.6-17.7 ms per A.x, C2 10.72-10.75 -> 10.17-10.26, headline neutral; two batches in
     // flight or ds_bpermute instead of DPP: within 1 %)
     if (ncomp == 4 && O <= 128) {
-      if (O <= 64) hipLaunchKernelGGL((k_xc_point_b<4, 1>), grid, blk, 0, st, G, g0, ngrid, nz, O, nmo, compP, pO0,
-                                      pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1);
-      else         hipLaunchKernelGGL((k_xc_point_b<4, 2>), grid, blk, 0, st, G, g0, ngrid, nz, O, nmo, compP, pO0,
-                                      pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1);
+      if (ns == 1) { if (O <= 64) XT_POINT_B(1, 1); else XT_POINT_B(2, 1); }
+      else         { if (O <= 64) XT_POINT_B(1, 2); else XT_POINT_B(2, 2); }
       return;
     }
-    if (ncomp == 4) XT_POINT(4, 4);
-    else            { if (O <= 64) XT_POINT(1, 1); else if (O <= 128) XT_POINT(1, 2); else XT_POINT(1, 4); }
+    if (ncomp == 4) { if (ns == 1) XT_POINT(4, 4, 1); else XT_POINT(4, 4, 2); }
+    else            { if (O <= 64) XT_POINT(1, 1, 2); else if (O <= 128) XT_POINT(1, 2, 2); else XT_POINT(1, 4, 2); }
 #undef XT_POINT
+#undef XT_POINT_B
     return;
   }
-  const bool same = (pO0 == pO1);
+  const bool same = (ns == 1 || pO0 == pO1);
   const size_t lds = (same ? 1 : 2) * (size_t)ncomp * O * sizeof(double);
-  if (ncomp == 4)
-    hipLaunchKernelGGL(k_xc_uks_w<4>, dim3(G), dim3(256), lds, st, g0, ngrid, nz, O, nmo, compP,
+  if (ncomp == 4 && ns == 1)
+    hipLaunchKernelGGL((k_xc_uks_w<4, 1>), dim3(G), dim3(256), lds, st, g0, ngrid, nz, O, nmo, compP,
+                       pO0, pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1);
+  else if (ncomp == 4)
+    hipLaunchKernelGGL((k_xc_uks_w<4, 2>), dim3(G), dim3(256), lds, st, g0, ngrid, nz, O, nmo, compP,
                        pO0, pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1);
   else
-    hipLaunchKernelGGL(k_xc_uks_w<1>, dim3(G), dim3(256), lds, st, g0, ngrid, nz, O, nmo, compP,
+    hipLaunchKernelGGL((k_xc_uks_w<1, 2>), dim3(G), dim3(256), lds, st, g0, ngrid, nz, O, nmo, compP,
                        pO0, pO1, wfxc, U0, ldU0, U1, ldU1, R0, ldR0, R1, ldR1);
 }
 void xc_sf(hipStream_t st, int G, int g0, int nz, int O, int nmo, const double* phio, const double* fsf, double* U) {
@@ -1177,8 +1194,8 @@ void xc_sf(hipStream_t st, int G, int g0, int nz, int O, int nmo, const double* 
   const int blocks = (int)((waves * 64 + 255) / 256);
   hipLaunchKernelGGL(k_xc_sf, dim3(blocks), dim3(256), 0, st, G, g0, nz, O, nmo, phio, fsf, U);
 }
-void weight_fxc(hipStream_t st, long n4, int ngrid, const double* w, double* f) {
-  hipLaunchKernelGGL(k_weight_fxc, dim3(nblocks(n4 * ngrid)), dim3(256), 0, st, n4, ngrid, w, f);
+void weight_fxc(hipStream_t st, long n4, int ngrid, double scale, const double* w, double* f) {
+  hipLaunchKernelGGL(k_weight_fxc, dim3(nblocks(n4 * ngrid)), dim3(256), 0, st, n4, ngrid, scale, w, f);
 }
 void xsf_assemble(hipStream_t st, int nz, int nc, int no, int nv, int remove, const double* vects, const double* z, double* ze) {
   const long n = (long)nz * (nc + no) * (no + nv);

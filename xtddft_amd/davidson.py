@@ -21,7 +21,11 @@ returning the 4-tuple ``(conv, e, x, icyc)`` its callers unpack
 * only the small ``heff`` (<= (max_space+nroots)^2) crosses to the host for
   ``scipy.linalg.eigh`` (Davidson.py:199), as in the reference.
 
-``aop`` receives and returns device tensors of shape (n, dim).  ``precond``
+``aop`` receives and returns device tensors of shape (n, dim).  Under a
+torch.distributed group (the replicated solver of a sharded operator) every
+iteration's decisions are gathered and compared across ranks
+(``parallel.lockstep_check``): a divergence raises on all ranks instead of
+leaving some waiting in the next all-reduce.  ``precond``
 may be a diagonal (array or device tensor: PySCF ``make_diag_precond`` with
 level shift 1e-3), a ``DiagPrecond`` (device kernel), or any host callable
 ``precond(dx, e, x0)`` (evaluated on host copies).
@@ -238,8 +242,13 @@ def restart_guess(path: str):
 def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e-14,
               max_memory=4000, dot=None, callback=None, nroots=1, lessio=False, pick=None,
               verbose=None, follow_state=False, tol_residual=None, fill_heff=None, device=0,
-              return_device=False):
+              return_device=False, lockstep=None):
+    """lockstep: None -- check the ranks' decisions whenever a process group of size > 1
+    is initialised; True / False to force."""
+    from .parallel import group_size, lockstep_check
     torch = _torch()
+    if lockstep is None:
+        lockstep = group_size() > 1
     if not torch.cuda.is_available():
         raise RuntimeError("xtddft_amd.davidson1 runs on the GPU; no device is visible")
     dev = _Dev(device)
@@ -330,6 +339,9 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
         dx_norm = np.sqrt(dev.norms2(r).cpu().numpy())
         for k in range(nr):
             conv[k] = abs(de[k]) < tol and dx_norm[k] < toloose
+        if lockstep:   # every break / restart decision below follows from these
+            lockstep_check(np.concatenate([[icyc, space, nnew, float(np.sum(heff[:space, :space]))],
+                                           e, dx_norm, conv]), f"iteration {icyc}")
         log.debug("davidson %d %d |r|=%.3g e=%s max|de|=%.3g", icyc, space, dx_norm.max(), e,
                   np.abs(de).max())
         if all(conv):
@@ -365,6 +377,8 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
             xt = rk
         else:
             xt = torch.empty((0, dim), dtype=torch.float64, device=dev.device)
+        if lockstep:
+            lockstep_check([icyc, xt.shape[0]], f"iteration {icyc} new vectors")
         if xt.shape[0] == 0:
             conv = dx_norm < toloose
             break

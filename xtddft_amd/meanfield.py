@@ -92,6 +92,10 @@ class MeanField:
                for LDA / GGA / MGGA (rho, grad rho, tau -- PySCF's MGGA layout).
     fxc_sf   : (ngrid,) ALDA0 spin-flip kernel already multiplied by the grid
                weight (``cache_xc_kernel_sf``, SF_TDA.py:82-84).
+    fxc_sf_mc: optional (nk, nk, ngrid) multicollinear spin-flip kernel (method=1,
+               ``cache_xc_kernel_sf_mc``, SF_TDA.py:942-974), un-weighted, over the spin
+               variables (s, grad s[, tau_s]); None: computed on demand from the SCF
+               density (``xtddft_amd.mcol.sf_mc_kernel``).
     xctype   : 'HF' | 'LDA' | 'GGA' | 'MGGA'
     omega, alpha, hyb : ``ni.rsh_and_hybrid_coeff`` (XTDA.py:501).
     """
@@ -106,6 +110,7 @@ class MeanField:
     grids: Optional[Grid] = None
     fxc: Optional[np.ndarray] = None
     fxc_sf: Optional[np.ndarray] = None
+    fxc_sf_mc: Optional[np.ndarray] = None
     cderi_lr: Optional[np.ndarray] = None
     xc: str = "synthetic"
     xctype: str = "GGA"

@@ -74,8 +74,11 @@ class DeviceOperator:
     def __init__(self, mf: MeanField, kind: str, *, sa: int = 0, foo: float = 1.0,
                  fglobal: float = 0.0, remove: bool = False, shard=(0, 1), device: int = 0,
                  stream=None, presharded=False, k_mode: str = "auto",
-                 k_max_gib: float = 0.0, replicate_df=None):
-        """presharded: True -- mf.cderi / mf.grids hold only this rank's slices;
+                 k_max_gib: float = 0.0, replicate_df=None, sf_kernel: str = "alda0", mc_kernel=None):
+        """sf_kernel: spin-flip XC kernel of the SF / XSF kinds -- 'alda0' (method 0,
+        mf.fxc_sf) or 'mc' (method 1: the multicollinear kernel ``mc_kernel`` (nk, nk, ngrid),
+        ``xtddft_amd.mcol.sf_mc_kernel``).
+        presharded: True -- mf.cderi / mf.grids hold only this rank's slices;
         "grid" -- only mf.grids is this rank's slice (mf.cderi is whole).
         k_mode: exchange evaluation ('auto' | 'direct' | 'stored', see
         xt_set_exchange_mode); k_max_gib caps the stored matrix in auto mode.
@@ -83,6 +86,12 @@ class DeviceOperator:
         window + exchange rows (default: k_mode != 'direct')."""
         L = _capi.lib()
         self.mf, self.kind = mf, kind
+        if sf_kernel not in _capi.SF_KERNEL:
+            raise ValueError(f"sf_kernel must be one of {sorted(_capi.SF_KERNEL)}")
+        self.sf_kernel = sf_kernel if kind in ("SF_DOWN", "SF_UP", "XSF") else "alda0"
+        self.mc_kernel = mc_kernel
+        if self.sf_kernel == "mc" and mf.xctype != "HF" and mc_kernel is None:
+            raise ValueError("sf_kernel='mc' needs the multicollinear kernel (mc_kernel)")
         rank, nranks = shard
         nc, no, nv, _ = shape_info(mf, kind)
         nmo = nc + no + nv
@@ -114,6 +123,7 @@ class DeviceOperator:
         d.remove = 1 if remove else 0
         d.add_local = 1 if rank == 0 else 0
         d.device = device
+        d.sf_kernel = _capi.SF_KERNEL[self.sf_kernel]
         self.desc = d
         h = ctypes.c_void_p()
         _capi.check(L.xt_create(ctypes.byref(d), ctypes.byref(h)), "xt_create")
@@ -212,9 +222,16 @@ class DeviceOperator:
         if g1 > g0:
             grids = mf.grids
             sf = self.kind in ("SF_DOWN", "SF_UP", "XSF")
-            ao = grids.ao[:1, g0:g1] if sf else grids.ao[:, g0:g1]
             w = grids.weights[g0:g1]
-            kern = mf.fxc_sf[g0:g1] if sf else mf.fxc[..., g0:g1]
+            if sf and self.sf_kernel == "mc":       # multicollinear: GGA-shaped one-channel kernel
+                ao = grids.ao[:(1 if mf.xctype == "LDA" else 4), g0:g1]
+                kern = self.mc_kernel[..., g0:g1]
+            elif sf:                                # ALDA0: density only
+                ao = grids.ao[:1, g0:g1]
+                kern = mf.fxc_sf[g0:g1]
+            else:
+                ao = grids.ao[:, g0:g1]
+                kern = mf.fxc[..., g0:g1]
             if _is_device(ao):       # AO values resident in HBM (device eval_ao): kernel data follows
                 torch = _torch()
                 w, kern = (x if _is_device(x) else torch.as_tensor(np.ascontiguousarray(x), device=ao.device)

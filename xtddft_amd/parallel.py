@@ -14,7 +14,12 @@ is SURVEY.md 8(e)'s contraction-dimension sharding:
   ``nccl`` backend, i.e. RCCL over xGMI on MI355X (``gloo`` on CPU in tests).
 
 The Davidson control flow is deterministic given identical inputs, so every
-rank runs it redundantly on the all-reduced sigma and stays in lockstep.
+rank runs it redundantly on the all-reduced sigma and stays in lockstep; that
+assumption is checked, not trusted: ``lockstep_check`` gathers every rank's
+decision data each iteration (heff checksum, Ritz values, residual norms, the
+convergence flags, the number of new vectors) and raises on every rank at once when
+they differ -- a diverged rank would otherwise leave the others waiting in the next
+all-reduce forever.
 """
 from __future__ import annotations
 
@@ -61,6 +66,38 @@ def allreduce_sigma(sigma, group=None):
         return sigma
     dist.all_reduce(sigma, group=group)
     return sigma
+
+
+class LockstepError(RuntimeError):
+    pass
+
+
+def group_size(group=None):
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1
+    return dist.get_world_size(group)
+
+
+def lockstep_check(values, what="", group=None):
+    """All-gather ``values`` (a flat float64 vector, same length on every rank) and
+    raise ``LockstepError`` on EVERY rank when any rank's copy differs bitwise from
+    rank 0's.  A no-op without a process group of size > 1."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    n = group_size(group)
+    if n <= 1:
+        return
+    v = torch.as_tensor(np.ascontiguousarray(np.asarray(values, dtype=np.float64).ravel()))
+    if dist.get_backend(group) == "nccl":      # RCCL gathers device tensors only
+        v = v.to(f"cuda:{torch.cuda.current_device()}")
+    out = [torch.empty_like(v) for _ in range(n)]
+    dist.all_gather(out, v, group=group)
+    ref = out[0].cpu().numpy().view(np.int64)
+    bad = [r for r in range(1, n) if not np.array_equal(out[r].cpu().numpy().view(np.int64), ref)]
+    if bad:
+        raise LockstepError(f"replicated Davidson diverged ({what}): ranks {bad} differ from rank 0")
 
 
 def require_group(nranks):

@@ -8,9 +8,13 @@
   ``davidson_process(mf, nstates, method, isf)`` (382-406, PySCF
   ``lib.davidson1`` with tol 1e-7, lindep 1e-14, max_cycle 3000).
 
-``method=0`` is the ALDA0 collinear-limit kernel (``mf.fxc_sf``), ``method=2``
-the collinear (no XC) response; ``method=1`` (multicollinear, needs mcfun)
-is outside the hot-path scope and raises.
+``method=0`` is the ALDA0 collinear-limit kernel (``mf.fxc_sf``), ``method=1``
+the multicollinear kernel (``_gen_uhf_tda_response_sf``, SF_TDA.py:855-1047; kernel
+from ``xtddft_amd.mcol.sf_mc_kernel``, response on the device's GGA / MGGA engine
+with one spin-flip channel), ``method=2`` the collinear (no XC) response.
+``collinear_samples`` defaults to the reference's per-path counts: 50 on the
+Davidson path (SF_TDA.py:219), 30 for the explicit matrix (``get_ab_sf``,
+SF_TDA.py:1051, 570, 843).
 """
 from __future__ import annotations
 
@@ -36,11 +40,22 @@ def mf_info(mf: MeanField):
     return np.array([mf.mo_energy, mf.mo_energy]), occ, np.array([mf.mo_coeff, mf.mo_coeff])
 
 
+DAVIDSON_SAMPLES = 50    # SF_TDA.py:219
+EXPLICIT_SAMPLES = 30    # get_ab_sf default, SF_TDA.py:1051
+
+
 def _check_method(method):
-    if method == 1:
-        raise NotImplementedError("multicollinear kernel (method=1) needs mcfun; outside hot-path scope")
-    if method not in (0, 2):
+    if method not in (0, 1, 2):
         raise ValueError("method must be 0 (ALDA0), 1 (multicollinear) or 2 (collinear)")
+
+
+def sf_operator(mf, kind, method, collinear_samples, device=0, shard=(0, 1), **kw):
+    """The device operator of a spin-flip kind with the XC kernel of ``method``."""
+    if method == 1:
+        from .mcol import sf_mc_kernel
+        kern = sf_mc_kernel(mf, collinear_samples, device=device)
+        return DeviceOperator(mf, kind, device=device, shard=shard, sf_kernel="mc", mc_kernel=kern, **kw)
+    return DeviceOperator(_collinear(mf) if method == 2 else mf, kind, device=device, shard=shard, **kw)
 
 
 def _collinear(mf):
@@ -65,11 +80,11 @@ def sf_hdiag(mf, isf):
     raise ValueError("isf must be -1 (down) or +1 (up)")
 
 
-def gen_tda_operation_sf(mf, isf, method=0, device=0, shard=(0, 1)):
+def gen_tda_operation_sf(mf, isf, method=0, device=0, shard=(0, 1), collinear_samples=DAVIDSON_SAMPLES):
     _check_method(method)
     hdiag = sf_hdiag(mf, isf)
     kind = 'SF_DOWN' if isf == -1 else 'SF_UP'
-    op = DeviceOperator(_collinear(mf) if method == 2 else mf, kind, device=device, shard=shard)
+    op = sf_operator(mf, kind, method, collinear_samples, device=device, shard=shard)
 
     def vind(zs0):
         if isinstance(zs0, (list, tuple)):
@@ -106,8 +121,10 @@ def deal_v_davidson(mf, v):
     return np.asarray(v)[order_sf_down(*_sf_shape(mf))]
 
 
-def davidson_process(mf, nstates, method, isf=-1, device=0, shard=(0, 1), return_operator=False):
-    vind, hdiag = gen_tda_operation_sf(mf, isf, method, device=device, shard=shard)
+def davidson_process(mf, nstates, method, isf=-1, device=0, shard=(0, 1), return_operator=False,
+                     collinear_samples=DAVIDSON_SAMPLES):
+    vind, hdiag = gen_tda_operation_sf(mf, isf, method, device=device, shard=shard,
+                                       collinear_samples=collinear_samples)
     x0 = init_guess(mf, nstates, isf)
     conv, e, x1, icyc = _dav.davidson1(vind, x0, hdiag, tol=1e-7, lindep=1e-14, nroots=nstates,
                                        max_cycle=3000, device=device)
@@ -133,10 +150,11 @@ def _dense(op):
 class _SFBase:
     isf = 0
 
-    def __init__(self, mf, method=0, davidson=True, device=0, shard=(0, 1)):
+    def __init__(self, mf, method=0, davidson=True, device=0, shard=(0, 1), collinear_samples=None):
         _check_method(method)
         self.mf = mf
         self.method = method
+        self.collinear_samples = collinear_samples
         self.davidson = davidson
         self.device = device
         self.shard = tuple(shard)
@@ -147,7 +165,8 @@ class _SFBase:
         """Explicit A through the device operator; SF-down in the reference's
         cv|co|ov|oo block order (SF_TDA_down.get_Amat, SF_TDA.py:746-801)."""
         vind, _ = gen_tda_operation_sf(self.mf, self.isf, self.method, device=self.device,
-                                       shard=self.shard)
+                                       shard=self.shard,
+                                       collinear_samples=self.collinear_samples or EXPLICIT_SAMPLES)
         A = _dense(vind.operator)
         if self.isf == -1:
             order = order_sf_down(self.nc, self.no, self.nv)
@@ -158,7 +177,8 @@ class _SFBase:
         self.nstates = nstates
         if self.davidson:
             self.e, self.v, self.converged, self._op = davidson_process(
-                self.mf, nstates, self.method, self.isf, self.device, self.shard, return_operator=True)
+                self.mf, nstates, self.method, self.isf, self.device, self.shard, return_operator=True,
+                collinear_samples=self.collinear_samples or DAVIDSON_SAMPLES)
         else:
             self.A = self.get_Amat()
             self.e, self.v = scipy.linalg.eigh(self.A)
@@ -198,9 +218,9 @@ class SF_TDA_down(_SFBase):
         return Ds, lines
 
 
-def SF_TDA(mf, isf=-1, davidson=True, method=0, device=0, shard=(0, 1)):
+def SF_TDA(mf, isf=-1, davidson=True, method=0, device=0, shard=(0, 1), collinear_samples=None):
     if isf == -1:
-        return SF_TDA_down(mf, method, davidson, device, shard)
+        return SF_TDA_down(mf, method, davidson, device, shard, collinear_samples)
     if isf == 1:
-        return SF_TDA_up(mf, method, davidson, device, shard)
+        return SF_TDA_up(mf, method, davidson, device, shard, collinear_samples)
     raise ValueError("isf must be -1 or 1")

@@ -10,7 +10,9 @@ structure the reference consumes:
 * a symmetric DF factor ``B[P,mu,nu] = sym(N) * exp(-|mu-nu|/50)`` whose
   ``sum_P B B`` is a PSD, 8-fold symmetric ERI tensor;
 * a grid with AO values/gradients, weights and an ``fxc`` kernel symmetric
-  under (s,x) <-> (t,y); an ALDA0 ``fxc_sf`` kernel (weighted).
+  under (s,x) <-> (t,y); an ALDA0 ``fxc_sf`` kernel (weighted) and a multicollinear
+  spin-flip kernel ``fxc_sf_mc`` (nk, nk, ngrid), symmetric, un-weighted (drawn from
+  its own stream, so the other tensors do not depend on it).
 
 Magnitudes are calibrated so that the response part of A is ~0.05-0.1 Ha
 against orbital gaps >= 0.25 Ha, giving a positive spectrum that the
@@ -80,6 +82,15 @@ def make_fxc(rng, ngrid, ncomp):
             f[s * ncomp, t * ncomp] = v
             f[t * ncomp, s * ncomp] = v
     return f.reshape(2, ncomp, 2, ncomp, ngrid)
+
+
+def make_fxc_sf_mc(rng, ngrid, nk):
+    """Multicollinear spin-flip kernel (nk, nk, ngrid) symmetric in (x, y); its (s, s)
+    entry negative like the collinear-limit kernel (v_a - v_b) / (2 s)."""
+    f = rng.standard_normal((nk, nk, ngrid)) * 0.01
+    f = 0.5 * (f + f.transpose(1, 0, 2))
+    f[0, 0] = -0.5 * rng.uniform(0.1, 1.0, ngrid)
+    return f
 
 
 def make_mf(nao=24, nc=5, no=2, naux=None, ngrid=None, xctype="GGA", hyb=0.2,
@@ -160,10 +171,13 @@ def make_mf(nao=24, nc=5, no=2, naux=None, ngrid=None, xctype="GGA", hyb=0.2,
     else:
         hyb, alpha, omega = 1.0, 0.0, 0.0
 
+    fxc_sf_mc = None
+    if xctype != "HF":
+        fxc_sf_mc = make_fxc_sf_mc(np.random.default_rng(seed + 17), ngrid, 5 if xctype == "MGGA" else ncomp)
     mol = Mole(nao=nao, spin=no, nelectron=2 * nc + no)
     return MeanField(mol=mol, mo_coeff=mo_coeff, mo_occ=mo_occ, mo_energy=mo_energy,
                      h1e=h1e, veff=veff, veff_hf=veff_hf, cderi=cderi, grids=grids,
-                     fxc=fxc, fxc_sf=fxc_sf, cderi_lr=cderi_lr, xctype=xctype,
+                     fxc=fxc, fxc_sf=fxc_sf, fxc_sf_mc=fxc_sf_mc, cderi_lr=cderi_lr, xctype=xctype,
                      omega=omega, alpha=alpha, hyb=hyb)
 
 
@@ -178,26 +192,42 @@ def as_eri8(mf: MeanField, chol_tol: float = 0.0) -> MeanField:
                                eri_lr=eri_lr, chol_tol=chol_tol)
 
 
+GRID_BLOCK = 65536     # grid points per generator block (make_device_mf)
+AUX_BLOCK = 64         # DF rows per generator block
+
+
+def _block_generator(dev, seed, stream, index):
+    """A generator for block ``index`` of stream ``stream`` (0: DF factor, 1: grid, 2: the
+    multicollinear kernel): every block has its own seed, so a block's values do not depend
+    on which rank generates it or on how the global range is split."""
+    import torch
+    g = torch.Generator(device=dev)
+    g.manual_seed((int(seed) * 1000003 + 7919 * (stream + 1) + 104729 * int(index)) % (1 << 62))
+    return g
+
+
 def make_device_mf(nao=1000, nc=99, no=2, naux=None, ngrid=None, xctype="GGA", hyb=0.2,
-                   seed=DEFAULT_SEED, device=0, shard=(0, 1), full_aux=False) -> MeanField:
+                   seed=DEFAULT_SEED, device=0, shard=(0, 1), full_aux=False, sf_mc=False,
+                   torch_device=None) -> MeanField:
     """Synthetic ROKS problem whose big tensors are generated directly in HBM.
 
-    Same distributions as ``make_mf`` (torch RNG, so not bitwise equal): the
-    DF factor and the grid are generated only for this rank's shard
-    (aux rows / grid points ``shard = (rank, nranks)``), scaled with the
-    GLOBAL sizes so every shard count describes the same operator statistics.
-    Small per-orbital data (C, Fock, energies) come from ``make_mf`` and are
-    identical on every rank.  full_aux: every rank generates the whole DF
-    factor (same values on all ranks; the replicated-factor partition).
+    Same distributions as ``make_mf`` (torch RNG, so not bitwise equal).  The DF factor
+    is generated in blocks of AUX_BLOCK rows and the grid in blocks of GRID_BLOCK points,
+    each block from its own seed (``_block_generator``): a rank generates only the blocks
+    of its shard (aux rows / grid points of ``shard = (rank, nranks)``) and the shards of
+    any rank count concatenate to the SAME global tensors -- a sharded run solves the
+    operator of the 1-GPU run.  Small per-orbital data (C, Fock, energies) come from
+    ``make_mf`` and are identical on every rank.  full_aux: every rank holds the whole DF
+    factor (the replicated-factor partition).  sf_mc: also a multicollinear spin-flip
+    kernel ``fxc_sf_mc`` (nk, nk, ngrid).  torch_device: generate on that torch device
+    instead of ``cuda:device`` (the shard-invariance test runs on the CPU).
     """
     import torch
     naux = naux if naux is not None else 3 * nao
     ngrid = ngrid if ngrid is not None else 1200 * nao
     rank, nranks = shard
     small = make_mf(nao=nao, nc=nc, no=no, naux=1, ngrid=1, xctype=xctype, hyb=hyb, seed=seed)
-    dev = torch.device(f"cuda:{device}")
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed + 7919 * (rank + 1))
+    dev = torch.device(torch_device) if torch_device is not None else torch.device(f"cuda:{device}")
     nv = nao - nc - no
 
     def split(n):
@@ -206,41 +236,57 @@ def make_device_mf(nao=1000, nc=99, no=2, naux=None, ngrid=None, xctype="GGA", h
         return lo, lo + base + (1 if rank < rem else 0)
     p0, p1 = (0, naux) if full_aux else split(naux)
     g0, g1 = split(ngrid)
-    gaux = g
-    if full_aux:       # rank-independent stream for the replicated factor
-        gaux = torch.Generator(device=dev)
-        gaux.manual_seed(seed + 104729)
     nocc, nvir = nc + no, no + nv
-    k = torch.arange(nao, device=dev, dtype=torch.float64)
+    f64 = dict(dtype=torch.float64, device=dev)
+    k = torch.arange(nao, **f64)
     dmat = torch.exp(-torch.abs(k[:, None] - k[None, :]) / 50.0)
-    s = df_scale(nao, naux, nocc, nvir) / np.sqrt(2.0)
-    cderi = torch.empty((p1 - p0, nao, nao), dtype=torch.float64, device=dev)
-    for q0 in range(0, p1 - p0, 64):
-        q1 = min(p1 - p0, q0 + 64)
-        t = torch.randn((q1 - q0, nao, nao), dtype=torch.float64, device=dev, generator=gaux)
-        cderi[q0:q1] = (t + t.transpose(1, 2)) * s * dmat
+    sdf = df_scale(nao, naux, nocc, nvir) / np.sqrt(2.0)
+    cderi = torch.empty((p1 - p0, nao, nao), **f64)
+    for b in range(p0 // AUX_BLOCK, -(-p1 // AUX_BLOCK)):
+        b0, b1 = b * AUX_BLOCK, min(naux, (b + 1) * AUX_BLOCK)
+        t = torch.randn((b1 - b0, nao, nao), generator=_block_generator(dev, seed, 0, b), **f64)
+        lo, hi = max(b0, p0), min(b1, p1)
+        cderi[lo - p0:hi - p0] = (t[lo - b0:hi - b0] + t[lo - b0:hi - b0].transpose(1, 2)) * sdf * dmat
         del t
     ncomp = 4 if xctype in ("GGA", "MGGA") else 1
     nf = 5 if xctype == "MGGA" else ncomp              # kernel components (+ tau)
     ng = g1 - g0
     scale = grid_scale(ngrid, nocc, nvir)
-    ao = torch.randn((ncomp, ng, nao), dtype=torch.float64, device=dev, generator=g)
-    ao.mul_(scale)
-    w = torch.rand(ng, dtype=torch.float64, device=dev, generator=g) / ngrid
+    ao = torch.empty((ncomp, ng, nao), **f64)
+    w = torch.empty(ng, **f64)
+    fxc = torch.empty((2, nf, 2, nf, ng), **f64)
+    fxc_sf = torch.empty(ng, **f64)
+    fmc = torch.empty((nf, nf, ng), **f64) if sf_mc else None
     n = 2 * nf
-    f = torch.randn((n, n, ng), dtype=torch.float64, device=dev, generator=g) * 0.01
-    f = 0.5 * (f + f.transpose(0, 1))
-    for sa in range(2):
-        for sb in range(2):
-            v = -(0.1 + 0.9 * torch.rand(ng, dtype=torch.float64, device=dev, generator=g))
-            f[sa * nf, sb * nf] = v
-            f[sb * nf, sa * nf] = v
-    fxc = f.reshape(2, nf, 2, nf, ng).contiguous()
-    fxc_sf = -(0.1 + 0.9 * torch.rand(ng, dtype=torch.float64, device=dev, generator=g)) * w
+    for b in range(g0 // GRID_BLOCK, -(-g1 // GRID_BLOCK)):
+        b0, b1 = b * GRID_BLOCK, min(ngrid, (b + 1) * GRID_BLOCK)
+        lo, hi = max(b0, g0), min(b1, g1)
+        nb, s0, s1, d0, d1 = b1 - b0, lo - b0, hi - b0, lo - g0, hi - g0
+        g = _block_generator(dev, seed, 1, b)
+        ao[:, d0:d1] = (torch.randn((ncomp, nb, nao), generator=g, **f64) * scale)[:, s0:s1]
+        wb = torch.rand(nb, generator=g, **f64) / ngrid
+        w[d0:d1] = wb[s0:s1]
+        f = torch.randn((n, n, nb), generator=g, **f64) * 0.01
+        f = 0.5 * (f + f.transpose(0, 1))
+        for sa in range(2):
+            for sb in range(2):
+                v = -(0.1 + 0.9 * torch.rand(nb, generator=g, **f64))
+                f[sa * nf, sb * nf] = v
+                f[sb * nf, sa * nf] = v
+        fxc[..., d0:d1] = f.reshape(2, nf, 2, nf, nb)[..., s0:s1]
+        fxc_sf[d0:d1] = (-(0.1 + 0.9 * torch.rand(nb, generator=g, **f64)) * wb)[s0:s1]
+        if sf_mc:
+            gm = _block_generator(dev, seed, 2, b)
+            m = torch.randn((nf, nf, nb), generator=gm, **f64) * 0.01
+            m = 0.5 * (m + m.transpose(0, 1))
+            m[0, 0] = -0.5 * (0.1 + 0.9 * torch.rand(nb, generator=gm, **f64))
+            fmc[..., d0:d1] = m[..., s0:s1]
+        del f
     small.cderi = cderi
     small.grids = Grid(ao=ao, weights=w)
     small.fxc = fxc
     small.fxc_sf = fxc_sf
+    small.fxc_sf_mc = fmc
     small.extra = dict(shard=shard, aux_range=(p0, p1), grid_range=(g0, g1), naux_global=naux,
                        ngrid_global=ngrid)
     return small

@@ -14,6 +14,8 @@ fglobal=None, fit=True)`` -> ``(e * 27.21138505, v)`` (XSF_TDA.py:1501-1554).
   of the reference's (nc*no + no*nv) unit-density J builds (859-913).
 * ``davidson_process`` uses the reference criteria tol 1e-8, lindep 1e-9,
   max_cycle 1000 (1467-1470) on the device solver.
+* ``method``: 0 ALDA0, 1 multicollinear (``collinear_samples`` Gauss-Legendre samples,
+  ``xtddft_amd.mcol``; fglobal fitted by 4 (cx - 1/2)^2, XSF_TDA.py:1517-1518), 2 collinear.
 """
 from __future__ import annotations
 
@@ -24,9 +26,8 @@ import scipy.linalg
 
 from . import davidson as _dav
 from .meanfield import MeanField
-from .operator import DeviceOperator
 from .parallel import require_group
-from .sf_tda import _check_method, _dense, mf_info
+from .sf_tda import _check_method, _dense, mf_info, sf_operator
 from .utils import HA2EV_XSF
 
 
@@ -112,8 +113,9 @@ class XSF_TDA:
         return f
 
     def _operator(self, foo, fglobal):
-        op = DeviceOperator(self.mf, 'XSF', sa=self.SA, foo=foo, fglobal=fglobal, remove=bool(self.re),
-                            device=self.device, shard=self.shard)
+        # method 1: the multicollinear response (XSF_TDA.py:1097-1098) with collinear_samples
+        op = sf_operator(self.mf, 'XSF', self.method, self.collinear_samples, device=self.device,
+                         shard=self.shard, sa=self.SA, foo=foo, fglobal=fglobal, remove=bool(self.re))
         if self.re:
             op.set_oo_basis(self.vects)
         return op
