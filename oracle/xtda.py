@@ -192,41 +192,42 @@ def full_diag_matrix(mf):
         bb -= np.einsum('ijba->iajb', eri_bb[:nocc_b, :nocc_b, nocc_b:, nocc_b:]) * c_lr
 
     if mf.xctype in ('LDA', 'GGA', 'MGGA'):
-        ao = mf.grids.ao
-        w = mf.grids.weights
-        fxc = mf.fxc
-        if mf.xctype == 'LDA':
-            wfxc = fxc[:, 0, :, 0] * w
-            rho_o_a = ao[0] @ orbo_a
-            rho_v_a = ao[0] @ orbv_a
-            rho_o_b = ao[0] @ orbo_b
-            rho_v_b = ao[0] @ orbv_b
-            rho_ov_a = np.einsum('ri,ra->ria', rho_o_a, rho_v_a)
-            rho_ov_b = np.einsum('ri,ra->ria', rho_o_b, rho_v_b)
-            aa += np.einsum('ria,rjb->iajb', rho_ov_a, rho_ov_a * wfxc[0, 0][:, None, None], optimize=True)
-            ab += np.einsum('ria,rjb->iajb', rho_ov_a, rho_ov_b * wfxc[0, 1][:, None, None], optimize=True)
-            bb += np.einsum('ria,rjb->iajb', rho_ov_b, rho_ov_b * wfxc[1, 1][:, None, None], optimize=True)
-        else:
-            wfxc = fxc * w
-            rho_o_a = np.einsum('xrp,pi->xri', ao, orbo_a)
-            rho_v_a = np.einsum('xrp,pi->xri', ao, orbv_a)
-            rho_o_b = np.einsum('xrp,pi->xri', ao, orbo_b)
-            rho_v_b = np.einsum('xrp,pi->xri', ao, orbv_b)
-            rho_ov_a = np.einsum('xri,ra->xria', rho_o_a, rho_v_a[0])
-            rho_ov_b = np.einsum('xri,ra->xria', rho_o_b, rho_v_b[0])
-            rho_ov_a[1:4] += np.einsum('ri,xra->xria', rho_o_a[0], rho_v_a[1:4])
-            rho_ov_b[1:4] += np.einsum('ri,xra->xria', rho_o_b[0], rho_v_b[1:4])
-            if mf.xctype == 'MGGA':     # tau_ov = 1/2 sum_c d_c phi_i d_c phi_a (XTDA.py:256-259)
-                tau_ov_a = np.einsum('xri,xra->ria', rho_o_a[1:4], rho_v_a[1:4]) * .5
-                tau_ov_b = np.einsum('xri,xra->ria', rho_o_b[1:4], rho_v_b[1:4]) * .5
-                rho_ov_a = np.vstack([rho_ov_a, tau_ov_a[np.newaxis]])
-                rho_ov_b = np.vstack([rho_ov_b, tau_ov_b[np.newaxis]])
+        # XTDA.py:178-276, summed over grid blocks (the whole-grid rho_ov of a 200-AO
+        # molecule would take tens of GB); each block's contraction as one GEMM
+        ng = mf.grids.ngrid
+        for g0 in range(0, ng, engines.GRID_BLOCK):
+            g1 = min(ng, g0 + engines.GRID_BLOCK)
+            ao = mf.grids.ao[:, g0:g1]
+            w = mf.grids.weights[g0:g1]
+            fxc = mf.fxc[..., g0:g1]
+            if mf.xctype == 'LDA':
+                wfxc = fxc[:, 0, :, 0] * w
+                rho_ov_a = np.einsum('ri,ra->ria', ao[0] @ orbo_a, ao[0] @ orbv_a)[None]
+                rho_ov_b = np.einsum('ri,ra->ria', ao[0] @ orbo_b, ao[0] @ orbv_b)[None]
+                wfxc = wfxc[:, None, :, None]
+            else:
+                wfxc = fxc * w
+                rho_o_a = np.einsum('xrp,pi->xri', ao, orbo_a)
+                rho_v_a = np.einsum('xrp,pi->xri', ao, orbv_a)
+                rho_o_b = np.einsum('xrp,pi->xri', ao, orbo_b)
+                rho_v_b = np.einsum('xrp,pi->xri', ao, orbv_b)
+                rho_ov_a = np.einsum('xri,ra->xria', rho_o_a, rho_v_a[0])
+                rho_ov_b = np.einsum('xri,ra->xria', rho_o_b, rho_v_b[0])
+                rho_ov_a[1:4] += np.einsum('ri,xra->xria', rho_o_a[0], rho_v_a[1:4])
+                rho_ov_b[1:4] += np.einsum('ri,xra->xria', rho_o_b[0], rho_v_b[1:4])
+                if mf.xctype == 'MGGA':     # tau_ov = 1/2 sum_c d_c phi_i d_c phi_a (XTDA.py:256-259)
+                    tau_ov_a = np.einsum('xri,xra->ria', rho_o_a[1:4], rho_v_a[1:4]) * .5
+                    tau_ov_b = np.einsum('xri,xra->ria', rho_o_b[1:4], rho_v_b[1:4]) * .5
+                    rho_ov_a = np.vstack([rho_ov_a, tau_ov_a[np.newaxis]])
+                    rho_ov_b = np.vstack([rho_ov_b, tau_ov_b[np.newaxis]])
             w_ov_aa = np.einsum('xyr,xria->yria', wfxc[0, :, 0], rho_ov_a)
             w_ov_ab = np.einsum('xyr,xria->yria', wfxc[0, :, 1], rho_ov_a)
             w_ov_bb = np.einsum('xyr,xria->yria', wfxc[1, :, 1], rho_ov_b)
-            aa += np.einsum('xria,xrjb->iajb', w_ov_aa, rho_ov_a, optimize=True)
-            bb += np.einsum('xria,xrjb->iajb', w_ov_bb, rho_ov_b, optimize=True)
-            ab += np.einsum('xria,xrjb->iajb', w_ov_ab, rho_ov_b, optimize=True)
+            ra = rho_ov_a.reshape(-1, nocc_a * nvir_a)       # (x r, i a)
+            rb = rho_ov_b.reshape(-1, nocc_b * nvir_b)
+            aa += (w_ov_aa.reshape(ra.shape).T @ ra).reshape(aa.shape)
+            bb += (w_ov_bb.reshape(rb.shape).T @ rb).reshape(bb.shape)
+            ab += (w_ov_ab.reshape(ra.shape).T @ rb).reshape(ab.shape)
 
     nc = min(nocc_a, nocc_b)
     no = abs(nocc_a - nocc_b)

@@ -92,6 +92,51 @@ def test_sf_tda_multicollinear_matches_oracle(torch, isf, kind):
     assert np.abs(np.asarray(e_ev) / HA2EV - w).max() < 1e-7
 
 
+@pytest.mark.parametrize("method", [0, 1])
+def test_xsf_get_sp_matches_oracle(torch, method):
+    """XSF_TDA(mf, calculate_sp=True).get_sp (XSF_TDA.py:215-262) on the triplet ROKS HF
+    molecule: the response element and the exchange integrals read off the device
+    operator equal the reference's own construction (gen_response_sf / get_k on |H><H|,
+    |L><L|, projected to MOs) through the oracle."""
+    import dataclasses
+    from oracle import engines
+    from xtddft_amd import XSF_TDA
+    from xtddft_amd.mcol import sf_mc_kernel
+    mf = hf_meanfield("ROKS")
+    x = XSF_TDA(mf, method=method, calculate_sp=True)
+    sp = x.sp
+    nc, no = x.nc, x.no
+    mfo = dataclasses.replace(mf, fxc_sf_mc=sf_mc_kernel(mf, 60) if method == 1 else None)
+    c = mf.mo_coeff
+    h, l = c[:, nc:nc + 1], c[:, nc + 1:nc + 2]
+    h_mo = c.T @ engines.gen_response_sf(mfo, method=method)((h @ h.T)[None])[0] @ c
+    assert abs(sp["lhhl"] - h_mo[nc + no, nc + no]) < 1e-12
+    for d, key in ((h @ h.T, "homo"), (l @ l.T, "lumo")):
+        k_mo = c.T @ engines.jk(mf, d[None], with_j=False)[1][0] @ c
+        assert np.abs(sp[key] - k_mo[:nc, nc + no:]).max() < 1e-12
+    assert len(sp["lines"]) == 2 + 4 * 11 + 1
+
+
+def test_xsf_frozen_core_matches_oracle(torch):
+    """kernel(frozen=...) with davidson=False on the UKS reference (XSF_TDA.py:1483-1499,
+    1544-1545): the explicit matrix without the frozen core rows, against the oracle's
+    explicit matrix sliced the same way."""
+    from oracle import xsf_tda as oxsf
+    from xtddft_amd import XSF_TDA
+    mf = hf_meanfield("UKS")
+    o = oxsf.XSFOracle(mf)
+    a_ref = o.get_amat(fglobal=oxsf.default_fglobal(mf))
+    nc, no, nv = o.nc, o.no, o.nv
+    for frozen, f in ((True, 1), (2, 2)):
+        x = XSF_TDA(mf, davidson=False)
+        e, _ = x.kernel(nstates=5, frozen=frozen)
+        m = a_ref[f * nv:, f * nv:]
+        kept = np.r_[0:(nc - f) * nv, (nc - f) * nv + f * no:m.shape[0]]
+        w = np.linalg.eigvalsh(m[np.ix_(kept, kept)])[:5]
+        assert x.A.shape == (m.shape[0] - f * no,) * 2
+        assert np.abs(np.asarray(e) / HA2EV_XSF - w).max() < 1e-10
+
+
 def test_xtda_on_roks_molecule_matches_oracle(torch):
     """X-TDA (XTDA.py:746-829) on the converged ROKS HF molecule: device Davidson
     roots equal the oracle's explicit-A eigenvalues (no reference printout exists

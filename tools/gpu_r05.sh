@@ -9,3 +9,7 @@ for c in ${BENCH:-}; do
   timeout -k 10 ${BLIMIT:-400} python -u bench.py --config $c ${BARGS:-} > gpurun_out/${T}_bench_$c.json 2> gpurun_out/${T}_bench_$c.err || { echo "bench $c failed"; tail -5 gpurun_out/${T}_bench_$c.err; exit 1; }
   python -c "import json,sys; d=json.load(open('gpurun_out/${T}_bench_$c.json')); print('$c', d['value'], d.get('verify',{}).get('rel_err'), d['roofline']['frac'], d.get('cpu_baseline',{}).get('value'))"
 done
+for m in ${MOLS:-}; do
+  timeout -k 10 ${MLIMIT:-600} python -u tools/molecule_run.py --molecule $m > gpurun_out/${T}_mol_$m.log 2>&1 || { echo "molecule $m failed"; tail -5 gpurun_out/${T}_mol_$m.log; exit 1; }
+  tail -1 gpurun_out/${T}_mol_$m.log | cut -c1-400
+done

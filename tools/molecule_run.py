@@ -1,0 +1,124 @@
+"""A BASELINE-class molecule end to end on the device, checked against the oracle.
+
+    python tools/molecule_run.py --molecule naphthalene+ [--nroots 20] [--out FILE]
+    python tools/molecule_run.py --molecule ch2
+
+* naphthalene+ : C10H8+ doublet, cc-pVDZ (180 AOs: the nao of BASELINE config C2's
+  def2-SVP), ROKS B3LYP (the reference's default functional, XTDA.py:1526), X-TDA 20 roots;
+* ch2          : CH2 3B1 triplet, 6-31G (13 AOs, BASELINE config C1), ROKS B3LYP, 5 roots.
+
+Pipeline: device integrals and AO values, the integral-direct pivoted Cholesky factor of
+the exact ERIs (no DF approximation: the reference's exact J/K), ROKS SCF on the device,
+then XTDA(mf).kernel() (device operator + device Davidson, XTDA.py:746-829).  Check: the
+device roots against the eigenvalues (w > 1e-3, XTDA.py:769-772) of the oracle's explicit
+X-TDA matrix (oracle.xtda.full_diag_matrix, XTDA.py:56-400) on the same mean field, and a
+residual |A x - e x| per root through a fresh device A.x.  Writes one JSON record.
+"""
+import argparse
+import dataclasses
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, ".."))
+
+# D2h naphthalene (Angstrom), long axis x, the fused C-C bond on the y axis
+NAPHTHALENE = """C 0.0000 0.7164 0; C 0.0000 -0.7164 0;
+C 1.2431 1.4002 0; C -1.2431 1.4002 0; C 1.2431 -1.4002 0; C -1.2431 -1.4002 0;
+C 2.4262 0.7081 0; C -2.4262 0.7081 0; C 2.4262 -0.7081 0; C -2.4262 -0.7081 0;
+H 1.2428 2.4878 0; H -1.2428 2.4878 0; H 1.2428 -2.4878 0; H -1.2428 -2.4878 0;
+H 3.3700 1.2434 0; H -3.3700 1.2434 0; H 3.3700 -1.2434 0; H -3.3700 -1.2434 0"""
+# CH2 3B1: C-H 1.075 A, H-C-H 133.9 degrees
+CH2 = "C 0 0 0; H 0 0.98934 -0.42079; H 0 -0.98934 -0.42079"
+
+MOLECULES = {
+    "naphthalene+": dict(atom=NAPHTHALENE, basis="cc-pvdz", charge=1, spin=1, nroots=20,
+                         label="naphthalene+ doublet / cc-pVDZ (BASELINE C2 class: nao 180)"),
+    "ch2": dict(atom=CH2, basis="6-31g", charge=0, spin=2, nroots=5,
+                label="CH2 3B1 / 6-31G (BASELINE C1)"),
+}
+
+
+def _host(x):
+    return x.cpu().numpy() if hasattr(x, "cpu") else np.asarray(x)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--molecule", default="naphthalene+", choices=sorted(MOLECULES))
+    ap.add_argument("--nroots", type=int, default=None)
+    ap.add_argument("--xc", default="b3lyp")
+    ap.add_argument("--tol", type=float, default=1e-12, help="Cholesky tolerance of the exact ERIs")
+    ap.add_argument("--conv", type=float, default=1e-10)
+    ap.add_argument("--no-oracle", action="store_true")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    spec = MOLECULES[a.molecule]
+    nroots = a.nroots or spec["nroots"]
+    import torch
+    from xtddft_amd.qc import M, ROKS
+    from xtddft_amd.xtda import XTDA
+    rec = dict(molecule=spec["label"], xc=a.xc, chol_tol=a.tol, nroots=nroots)
+    t0 = time.perf_counter()
+    mol = M(spec["atom"], basis=spec["basis"], charge=spec["charge"], spin=spec["spin"])
+    rec.update(nao=mol.nao, natm=mol.natm, nelectron=mol.nelectron)
+    mf = ROKS(mol, a.xc)
+    mf.conv_tol = a.conv
+    mf.max_cycle = 200
+    mf.to_device(0).cholesky(a.tol)
+    mf.build()
+    torch.cuda.synchronize()
+    rec["build_s"] = round(time.perf_counter() - t0, 3)
+    rec["build_phases_s"] = {k: round(v, 3) for k, v in mf.timings.items()}
+    rec["ngrid"] = int(mf.grids.size)
+    print("build", json.dumps(rec), flush=True)
+    t0 = time.perf_counter()
+    mf.kernel()
+    torch.cuda.synchronize()
+    rec.update(scf_s=round(time.perf_counter() - t0, 3), scf_converged=bool(mf.converged), e_tot=mf.e_tot)
+    print("scf", rec["scf_s"], mf.converged, mf.e_tot, flush=True)
+    t0 = time.perf_counter()
+    mfield = mf.to_meanfield()
+    torch.cuda.synchronize()
+    rec["meanfield_s"] = round(time.perf_counter() - t0, 3)
+    td = XTDA(None, mfield, nstates=nroots)
+    t0 = time.perf_counter()
+    e = np.asarray(td.kernel())
+    torch.cuda.synchronize()
+    op = td.operator()
+    rec.update(xtda_s=round(time.perf_counter() - t0, 3), xtda_converged=bool(np.all(td.converged)),
+               operator_setup_s={k: round(v, 3) for k, v in op.setup_s.items()},
+               dim=int(op.dim), k_mode=op.k_mode, naux_cholesky=op.naux()[0],
+               roots_ha=[float(x) for x in e])
+    x = td.v[np.argsort(td.order), :].T          # back to PySCF order
+    ax = op.apply(np.ascontiguousarray(x))
+    rec["max_residual"] = float(np.linalg.norm(ax - e[:, None] * x, axis=1).max())
+    print("xtda", rec["xtda_s"], rec["dim"], e[:5], flush=True)
+    if not a.no_oracle:
+        from oracle import xtda as oxtda
+        from xtddft_amd.meanfield import Grid
+        t0 = time.perf_counter()
+        mfo = dataclasses.replace(mfield, cderi=_host(mfield.cderi),
+                                  grids=Grid(ao=_host(mfield.grids.ao), weights=_host(mfield.grids.weights)),
+                                  fxc=_host(mfield.fxc))
+        A = oxtda.full_diag_matrix(mfo)
+        rec["oracle_symmetry"] = float(np.abs(A - A.T).max() / np.abs(A).max())
+        w = np.linalg.eigvalsh(0.5 * (A + A.T))
+        w = w[w > 1e-3][:nroots]
+        rec["oracle_s"] = round(time.perf_counter() - t0, 1)
+        rec["oracle_roots_ha"] = [float(v) for v in w]
+        rec["max_abs_diff_ha"] = float(np.abs(e - w).max())
+        print("oracle", rec["oracle_s"], rec["max_abs_diff_ha"], flush=True)
+    out = a.out or f"gpurun_out/molecule_{a.molecule.replace('+', 'p')}.json"
+    os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
+    with open(out, "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

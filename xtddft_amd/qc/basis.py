@@ -23,6 +23,18 @@ _631G = {
     ],
 }
 
+# 6-31G carbon (Hehre, Ditchfield, Pople, J. Chem. Phys. 56, 2257 (1972); the EMSL / NWChem
+# values PySCF ships) -- not printed by any reference run: BASELINE config C1 (CH2 3B1 /
+# 6-31G) is checked device against oracle (tools/molecule_run.py), not against the reference.
+_631G["C"] = [
+    [0, [3047.5249, 0.0018347], [457.36951, 0.0140373], [103.94869, 0.0688426],
+     [29.210155, 0.2321844], [9.286663, 0.4679413], [3.163927, 0.3623120]],
+    [0, [7.8682724, -0.1193324], [1.8812885, -0.1608542], [0.5442493, 1.1434564]],
+    [0, [0.1687144, 1.0]],
+    [1, [7.8682724, 0.0689991], [1.8812885, 0.3164240], [0.5442493, 0.7443083]],
+    [1, [0.1687144, 1.0]],
+]
+
 # STO-3G hydrogen (zeta = 1.24), the Szabo-Ostlund textbook H2 basis used by the
 # integral unit tests.
 _STO3G = {

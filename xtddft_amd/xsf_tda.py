@@ -16,6 +16,11 @@ fglobal=None, fit=True)`` -> ``(e * 27.21138505, v)`` (XSF_TDA.py:1501-1554).
   max_cycle 1000 (1467-1470) on the device solver.
 * ``method``: 0 ALDA0, 1 multicollinear (``collinear_samples`` Gauss-Legendre samples,
   ``xtddft_amd.mcol``; fglobal fitted by 4 (cx - 1/2)^2, XSF_TDA.py:1517-1518), 2 collinear.
+* ``calculate_sp=True`` runs ``get_sp`` (XSF_TDA.py:215-262): the spin-polarisation
+  integrals of a triplet reference, <LH|HL> and <iH|Ha>, <iL|La>, as elements of the
+  device operator's response to the unit H->H / L->L spin flips.
+* ``kernel(frozen=...)`` drops frozen core orbitals from the explicit matrix
+  (``frozen_A``, XSF_TDA.py:1483-1499, 1544-1545: davidson=False without OO removal).
 """
 from __future__ import annotations
 
@@ -97,11 +102,86 @@ class XSF_TDA:
             self.omega, self.alpha, self.hyb = mf.omega, mf.alpha, mf.hyb
         _, dsp1 = mf.spin_square()
         self.ground_s = (dsp1 - 1) / 2
-        if calculate_sp:
-            raise NotImplementedError("spin-polarisation analysis (get_sp) is post-processing, out of scope")
         self.re = None
+        self.calculate_sp = calculate_sp
+        if calculate_sp:   # J. Chem. Theory Comput. 2023, 19, 7606-7616 (XSF_TDA.py:211-213)
+            self.sp = self.get_sp()
 
     # ------------------------------------------------------------ helpers
+    def get_sp(self, verbose=True):
+        """Spin-polarisation analysis of a triplet ROKS reference (XSF_TDA.py:215-262): the
+        response V[|H><H|] of the spin-flip kernel (XC of ``method`` + hybrid exchange,
+        ``gen_response_sf``) at MO element (nc + no, nc + no) -- what the reference prints as
+        <LH|HL> -- and the pure exchange integrals <iH|Ha> = K[|H><H|]_ia, <iL|La> =
+        K[|L><L|]_ia (core i, virtual a; H, L the two open shells).  Each is read off one
+        device A.x on a unit spin-flip vector: <iH|Ha>, <iL|La> from an exchange-only
+        operator, the response element from one whose occupied space is widened by one
+        orbital so that (nc + no, nc + no) is a spin-flip pair (the Fock terms vanish at
+        all these elements).  Returns dict(lhhl, homo (nc, nv), lumo (nc, nv)) and prints
+        the reference's top-10 tables."""
+        import dataclasses
+        from .operator import DeviceOperator
+        from .sf_tda import _collinear
+        if self.type_u or self.no != 2:
+            raise ValueError("get_sp analyses a triplet ROKS reference (two open shells)")
+        nc, no, nv = self.nc, self.no, self.nv
+        mf = self.mf
+
+        def unit(dim, nvb, i, a):   # SF-down vector in PySCF order (occ_a x vir_b)
+            z = np.zeros((1, dim))
+            z[0, i * nvb + a] = 1.0
+            return z
+        # response at (nc + no, nc + no): occupations widened by that orbital (order kept:
+        # core | open | virtual), kernel and orbitals unchanged
+        occ = np.array(mf.mo_occ, dtype=np.float64)
+        occ[nc + no] = 1.0
+        wide = dataclasses.replace(mf, mo_occ=occ)
+        if self.method == 1:
+            from .mcol import sf_mc_kernel
+            resp = DeviceOperator(wide, "SF_DOWN", device=self.device, sf_kernel="mc",
+                                  mc_kernel=sf_mc_kernel(mf, self.collinear_samples, device=self.device))
+        else:
+            resp = DeviceOperator(_collinear(wide) if self.method == 2 else wide, "SF_DOWN", device=self.device)
+        nvb = no + 1 + nv - 1
+        lhhl = float(resp.apply(unit(resp.dim, nvb, nc, 0))[0, (nc + no) * nvb + no])
+        resp.close()
+        kmf = dataclasses.replace(mf, xctype="HF", hyb=1.0, alpha=0.0, omega=0.0, grids=None, fxc=None,
+                                  fxc_sf=None, fxc_sf_mc=None, cderi_lr=None, eri_lr=None)
+        kop = DeviceOperator(kmf, "SF_DOWN", device=self.device)
+        nvb = no + nv
+        homo = -kop.apply(unit(kop.dim, nvb, nc, 0))[0].reshape(nc + no, nvb)[:nc, no:]
+        lumo = -kop.apply(unit(kop.dim, nvb, nc + 1, 1))[0].reshape(nc + no, nvb)[:nc, no:]
+        kop.close()
+
+        def top10(m):
+            idx = np.argsort(-np.abs(m), axis=None)[:10]
+            return [(float(m.flat[k]),) + tuple(int(t) for t in np.unravel_index(k, m.shape)) for k in idx]
+        lines = ["=================================================", f"<LH|HL> is {lhhl:9.6f}"]
+        for title, m in (("<iH|Ha>", homo), ("<iL|La>", lumo), ("<iH|Ha>-<iL|La>", homo - lumo),
+                         ("<iH|Ha>*<iL|La>", homo * lumo)):
+            lines.append(f"Top 10 value in {title}:")
+            for n, (v, i, a) in enumerate(top10(m)):
+                lines.append(f"{n + 1} {v:9.6f}, CV is {(i + 1, a + nc + no + 1)}")
+        lines.append("=================================================")
+        if verbose:
+            print("\n".join(lines))
+        return dict(lhhl=lhhl, homo=homo, lumo=lumo, lines=lines)
+
+    def frozen_A(self, frozen):
+        """Drop frozen core orbitals from the un-compressed cv|co|ov|oo matrix
+        (XSF_TDA.py:1483-1499): ``frozen=True`` drops the innermost core orbital, an
+        integer n > 0 the n innermost (the reference's integer branch reads ``f`` before
+        assigning it; n is what it means)."""
+        f = frozen if (isinstance(frozen, (int, np.integer)) and not isinstance(frozen, bool)
+                       and frozen > 0) else 1
+        nc, no, nv = self.nc, self.no, self.nv
+        if f > nc:
+            raise ValueError(f"cannot freeze {f} of {nc} core orbitals")
+        minus_cv = self.A[f * nv:, f * nv:]
+        dim = minus_cv.shape[0]
+        kept = np.r_[0:(nc - f) * nv, (nc - f) * nv + f * no:dim]
+        return minus_cv[np.ix_(kept, kept)]
+
     def get_vect(self):
         return get_vect(self.no)
 
@@ -223,8 +303,6 @@ class XSF_TDA:
         return _dense(vind.operator)
 
     def kernel(self, nstates=1, remove=None, frozen=None, foo=1.0, d_lda=0.3, fglobal=None, fit=True):
-        if frozen is not None:
-            raise NotImplementedError("frozen-orbital XSF (frozen_A) is outside the hot path")
         self.re = (not self.type_u) if remove is None else bool(remove)
         if self.re and self.no < 1:
             raise ValueError("OO compression needs an open shell")
@@ -237,6 +315,8 @@ class XSF_TDA:
             self.davidson_process(foo=foo, fglobal=fglobal)
         else:
             self.A = self.get_Amat(foo=foo, fglobal=fglobal)
+            if frozen is not None and not self.re:   # XSF_TDA.py:1544-1545 (the un-removed branch)
+                self.A = self.frozen_A(frozen)
             e, v = scipy.linalg.eigh(self.A)
             self.e = e[:self.nstates]
             self.v = v[:, :self.nstates]
