@@ -135,7 +135,11 @@ int xt_set_oo_basis(xt_ctx* ctx, const double* vects, int ptr_kind);
 int xt_set_exchange_mode(xt_ctx* ctx, int mode, double max_gib);
 /* Build what is built once per solve (the stored exchange matrix when the
    mode resolves to it; xt_apply would otherwise build it on first use) and
-   report the resolved mode and its HBM footprint (GiB). */
+   report the resolved mode and its HBM footprint (GiB).  A partitioned context
+   (xt_set_partition with a proper aux window) that stores the exchange then drops
+   the MO-factor rows outside its window (every later use reads only the window):
+   xt_naux reports the window; re-partitioning or a stored-exchange rebuild needs
+   the factor set again. */
 int xt_prepare(xt_ctx* ctx, int* k_mode, double* k_gib);
 
 /* Rank partition of a sharded operator (one process per GPU):

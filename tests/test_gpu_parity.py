@@ -319,3 +319,27 @@ def test_sf_multicollinear_many_occupied(dev, nc):
     z = make_trial_vectors(3, hdiag.size)
     op = dev(mf, "SF_DOWN", sf_kernel="mc", mc_kernel=mf.fxc_sf_mc)
     assert rel(op.apply(z), vind(z)) < RTOL
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_partitioned_stored_exchange_many_rows(hiplib, nranks):
+    """Stored exchange over a replicated factor with >= 2 KX_FOLD chunks of occupied rows
+    per rank (O = 48 over 2 and 3 ranks): the symmetric build's mirror runs for row blocks
+    that start past 0 (i0 > 0), and each partitioned context drops the factor rows outside
+    its aux window after the build (xt_prepare).  The summed parts equal the full operator
+    and the oracle."""
+    from xtddft_amd.operator import DeviceOperator
+    mf = make_mf(nao=80, nc=46, no=2, xctype="GGA", hyb=0.25, ngrid=2000)
+    vind, hdiag = oxtda.gen_tda_operation(mf)
+    z = make_trial_vectors(4, hdiag.size)
+    full = DeviceOperator(mf, "XTDA", k_mode="stored")
+    parts = [DeviceOperator(mf, "XTDA", k_mode="stored", shard=(r, nranks), replicate_df=True)
+             for r in range(nranks)]
+    assert all(p.k_mode == "stored" for p in parts)
+    rows = [p.partition["exchange_rows"] for p in parts]
+    assert all(i1 - i0 >= 2 * 8 for i0, i1 in rows) and rows[-1][0] > 0
+    win = [p.partition["aux"] for p in parts]
+    assert [p.naux()[0] for p in parts] == [p1 - p0 for p0, p1 in win]   # factor trimmed to the window
+    s = sum(p.apply(z) for p in parts)
+    assert rel(s, full.apply(z)) < RTOL
+    assert rel(s, vind(z)) < RTOL

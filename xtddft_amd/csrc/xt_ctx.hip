@@ -98,7 +98,18 @@ struct xt_ctx {
   bool m_kernel = true;          // XC M-backward through xt_xcm.hip (XT_M_KERNEL=0: the engine's mode 2)
   int w_kernel = 2;              // XC rho-forward: 1 xt_xcw.hip, 0 the engine's mode 1, 2 by size (XT_W_KERNEL)
   int kr0 = 0, kr1 = -1;         // -1: all O rows
+  bool trimmed = false;          // the MO factor holds only this rank's aux window (xt_prepare)
+  int naux_full = 0;             // desc naux before the trim
 };
+
+// a factor setter after a trim starts over with the full aux count (both factors must be set again)
+static void untrim(xt_ctx* c) {
+  if (!c->trimmed) return;
+  c->d.naux = c->naux_full;
+  c->Bmo.release(); c->Bmo_lr.release();
+  c->has_df = c->has_lr = false;
+  c->trimmed = false;
+}
 
 static int dim_of(const xt_desc& d) {
   const int nc = d.nc, no = d.no, nv = d.nv;
@@ -383,6 +394,7 @@ int xt_set_jk_df(xt_ctx* c, const double* cderi, int which, int ptr_kind) {
   if (which != 0 && which != 1) return fail(XT_ERR_ARG, "which must be 0 (full range) or 1 (long range)");
   if (!c->has_orb) return fail(XT_ERR_STATE, "xt_set_orbitals must precede xt_set_jk_df");
   (void)hipSetDevice(c->d.device);
+  untrim(c);
   DevBuf& dst = which == 0 ? c->Bmo : c->Bmo_lr;
   RET(df_to_mo(c, cderi, c->d.naux, dst, c->d.naux, ptr_kind));
   HIPCHK(hipStreamSynchronize(c->st));
@@ -415,6 +427,7 @@ int xt_set_jk_eri8(xt_ctx* c, const double* eri, int which, double tol, int p_ra
   if (p_count < 1 || p_rank < 0 || p_rank >= p_count) return fail(XT_ERR_ARG, "bad shard (p_rank, p_count)");
   if (!c->has_orb) return fail(XT_ERR_STATE, "xt_set_orbitals must precede xt_set_jk_eri8");
   (void)hipSetDevice(c->d.device);
+  untrim(c);
   const int nao = c->d.nao;
   const long npair = (long)nao * (nao + 1) / 2;
   const size_t n8 = (size_t)npair * (npair + 1) / 2;
@@ -772,6 +785,7 @@ static bool has_exchange(const xt_ctx* c) {
 
 extern "C" int xt_set_partition(xt_ctx* c, int p0, int p1, int i0, int i1) {
   if (!c) return fail(XT_ERR_ARG, "null ctx");
+  if (c->trimmed) return fail(XT_ERR_STATE, "the MO factor was trimmed to this rank's aux window; set it again");
   if (p0 < 0 || p1 < p0 || p1 > c->d.naux) return fail(XT_ERR_ARG, "aux window outside [0, naux]");
   if (i0 < 0 || i1 < i0 || i1 > c->O) return fail(XT_ERR_ARG, "exchange rows outside [0, O]");
   c->win_p0 = p0; c->win_np = p1 - p0;
@@ -804,6 +818,7 @@ static int resolve_kmode(xt_ctx* c) {
 constexpr int KX_FOLD = 8;
 
 static int build_kx(xt_ctx* c) {
+  if (c->trimmed) return fail(XT_ERR_STATE, "the stored exchange needs every aux row: set the factor again");
   const int O = c->O, V = c->V, nmo = c->d.nmo, naux = c->d.naux;
   const long mm = (long)nmo * nmo;
   const size_t ov = (size_t)O * V, ld = kx_ld(c);
@@ -960,12 +975,38 @@ extern "C" int xt_set_exchange_mode(xt_ctx* c, int mode, double max_gib) {
   return 0;
 }
 
+// Once a partitioned context holds its rows of the stored exchange, only the aux window
+// [win_p0, win_p0 + win_np) of the MO factor is ever read again (J, the XSF Delta-A, the
+// preconditioner diagonals): the other rows are dropped, so a replicated factor costs
+// naux / N rows per rank instead of naux (24 GB -> 3 GB at the headline, N = 8).
+static int trim_factor(xt_ctx* c) {
+  const size_t mm = (size_t)c->d.nmo * c->d.nmo;
+  const int np = c->win_np, p0 = c->win_p0, naux = c->d.naux;
+  DevBuf* bufs[2] = {&c->Bmo, &c->Bmo_lr};
+  for (DevBuf* B : bufs) {
+    if (!B->p) continue;
+    TmpBuf nb;
+    RET(nb.ensure((size_t)c->nbasis * np * mm));
+    for (int b = 0; b < c->nbasis; ++b)
+      HIPCHK(hipMemcpyAsync(nb.p + (size_t)b * np * mm, B->p + ((size_t)b * naux + p0) * mm, (size_t)np * mm * 8,
+                            hipMemcpyDeviceToDevice, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    nb.swap(*B);   // B takes the window, nb frees the full factor
+  }
+  c->naux_full = naux;
+  c->d.naux = np;
+  c->win_p0 = 0; c->win_np = -1;
+  c->trimmed = true;
+  return 0;
+}
+
 extern "C" int xt_prepare(xt_ctx* c, int* k_mode, double* k_gib) {
   if (!c) return fail(XT_ERR_ARG, "null ctx");
   (void)hipSetDevice(c->d.device);
   if (has_exchange(c) && !c->has_df) return fail(XT_ERR_STATE, "DF factor not set");
   RET(resolve_kmode(c));
   if (c->k_resolved == 1 && !c->kx_valid) RET(build_kx(c));
+  if (c->k_resolved == 1 && c->kx_valid && c->win_np > 0 && c->win_np < c->d.naux) RET(trim_factor(c));
   if (k_mode) *k_mode = c->k_resolved == 1 ? XT_K_STORED : XT_K_DIRECT;
   if (k_gib) *k_gib = c->k_resolved == 1 ? kx_doubles(c) * 8.0 / (double)((size_t)1 << 30) : 0.0;
   return 0;
