@@ -43,6 +43,12 @@ MOLECULES = {
 }
 
 
+def _rounded(d):
+    if isinstance(d, dict):
+        return {k: _rounded(v) for k, v in d.items()}
+    return round(d, 3) if isinstance(d, float) else d
+
+
 def _host(x):
     return x.cpu().numpy() if hasattr(x, "cpu") else np.asarray(x)
 
@@ -73,7 +79,7 @@ def main():
     mf.build()
     torch.cuda.synchronize()
     rec["build_s"] = round(time.perf_counter() - t0, 3)
-    rec["build_phases_s"] = {k: round(v, 3) for k, v in mf.timings.items()}
+    rec["build_phases_s"] = _rounded(dict(mf.timings))
     rec["ngrid"] = int(mf.grids.size)
     print("build", json.dumps(rec), flush=True)
     t0 = time.perf_counter()
@@ -91,7 +97,7 @@ def main():
     torch.cuda.synchronize()
     op = td.operator()
     rec.update(xtda_s=round(time.perf_counter() - t0, 3), xtda_converged=bool(np.all(td.converged)),
-               operator_setup_s={k: round(v, 3) for k, v in op.setup_s.items()},
+               operator_setup_s=_rounded(dict(op.setup_s)),
                dim=int(op.dim), k_mode=op.k_mode, naux_cholesky=op.naux()[0],
                roots_ha=[float(x) for x in e])
     x = td.v[np.argsort(td.order), :].T          # back to PySCF order
