@@ -50,7 +50,10 @@ sys.path.insert(0, ROOT)
 
 FP64_PEAK_TFLOPS = 78.6     # MI355X dense FP64 matrix peak (AMD spec); 74.2 measured (tools/mfma_probe.hip)
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8.0 TB/s spec
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04_pmc_summary.json")
+# the newest committed rocprofv3 FETCH / WRITE summary (tools/parse_prof.py)
+PMC_SUMMARY = next((os.path.join(ROOT, "profiles", f"r0{k}_pmc_summary.json") for k in (5, 4)
+                    if os.path.exists(os.path.join(ROOT, "profiles", f"r0{k}_pmc_summary.json"))),
+                   os.path.join(ROOT, "profiles", "r04_pmc_summary.json"))
 
 KIND_NAME = {"XTDA": "X-TDA", "SF_UP": "SF-TDA (spin-flip up)", "SF_DOWN": "SF-TDA (spin-flip down)",
              "XSF": "XSF-TDA"}
@@ -470,7 +473,7 @@ def converge(args, w, allreduce):
 # ---------------------------------------------------------------------------
 def load_traffic(config, tag_name):
     """HBM bytes per launch of the tagged kernel from this config's committed
-    rocprofv3 PMC summary (profiles/r04_pmc_summary.json), None if absent."""
+    rocprofv3 PMC summary (the newest profiles/r0*_pmc_summary.json), None if absent."""
     try:
         with open(PMC_SUMMARY) as f:
             d = json.load(f)
