@@ -4,12 +4,14 @@ its 160-row streaming tile and its batching.
 
 Automatic selection (xt_ctx.hip): the dedicated M-backward kernel (xt_xcm.hip) for
 O <= 128 and the generic engine's fused mode 2 above; the dedicated rho-forward
-kernel (xt_xcw.hip) for O >= 96 and the engine's fused mode 1 below, where it wins.
+kernel (xt_xcw.hip) for O >= 96, the small-O rho-forward kernel (xt_xcws.hip) for
+O <= 48 from 8 trial pairs, and the engine's fused mode 1 in between.
 The two test hooks (environment, read once at xt_create) force either side outside
 its automatic range so each path is checked at every occupied-row shape:
 
 * XT_M_KERNEL=0 -> XC M-backward through the engine's mode 2
-* XT_W_KERNEL=0 / 1 -> XC rho-forward through the engine's mode 1 / the dedicated kernel
+* XT_W_KERNEL=0 / 1 / 3 -> XC rho-forward through the engine's mode 1 / the O >= 96
+  kernel / the small-O kernel (every pair count; O <= 48)
 
 Tolerance: 1e-12 relative max-norm on sigma (FP64 round-off of a different
 summation order), as in test_gpu_parity.py.
@@ -48,7 +50,7 @@ def env():
 
 
 @pytest.mark.parametrize("knobs", [dict(), dict(XT_M_KERNEL=0), dict(XT_W_KERNEL=0), dict(XT_M_KERNEL=0, XT_W_KERNEL=0),
-                                   dict(XT_M_KERNEL=1, XT_W_KERNEL=1)])
+                                   dict(XT_M_KERNEL=1, XT_W_KERNEL=1), dict(XT_W_KERNEL=3)])
 @pytest.mark.parametrize("nc,no,nao", [(5, 2, 26), (33, 1, 60), (35, 2, 70), (95, 2, 130), (99, 2, 140),
                                       (120, 3, 150)])
 def test_xc_kernel_variants(hiplib, env, knobs, nc, no, nao):
@@ -109,7 +111,7 @@ def test_stored_exchange_small_row_counts(hiplib, kind, nz):
 
 @pytest.mark.parametrize("nz", [1, 2, 3, 5, 7, 13])
 @pytest.mark.parametrize("nc,no,nao", [(5, 2, 26), (33, 1, 60), (95, 2, 130), (99, 2, 140), (120, 3, 150)])
-@pytest.mark.parametrize("knobs", [dict(), dict(XT_W_KERNEL=1)])
+@pytest.mark.parametrize("knobs", [dict(), dict(XT_W_KERNEL=1), dict(XT_W_KERNEL=3)])
 def test_xc_kernels_small_batches(hiplib, env, knobs, nz, nc, no, nao):
     """Davidson steps with few new vectors: nx = 2 nz = 2, 4, 6, 10, 14, 26 trial pairs
     take the dedicated kernels' small-batch shapes (rho-forward: 8, 4, 2 or 1 pairs per

@@ -24,7 +24,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_lib")
 OBJ_DIR = os.path.join(OUT_DIR, "obj")
 OUT = os.path.join(OUT_DIR, "libxtddft_amd.so")
-SOURCES = ["xt_gemm.hip", "xt_exch.hip", "xt_xcm.hip", "xt_xcw.hip", "xt_kernels.hip", "xt_chol.hip", "xt_int.hip",
+SOURCES = ["xt_gemm.hip", "xt_exch.hip", "xt_xcm.hip", "xt_xcw.hip", "xt_xcws.hip", "xt_kernels.hip", "xt_chol.hip", "xt_int.hip",
            "xt_ctx.hip"]
 HEADERS = ["xt_internal.h", "xt_kernels.h", "../../include/xtddft_amd.h"]
 ARCH = os.environ.get("XT_OFFLOAD_ARCH", "gfx950")

@@ -251,12 +251,14 @@ int xt_create(const xt_desc* desc, xt_ctx** out) {
   {
     // the only environment knobs, read here once per context: which XC kernels run the
     // fused classes outside their automatic ranges (tests/test_gpu_variants.py).
-    // Defaults: dedicated M-backward for O <= 128 and rho-forward for O >= 96, the
-    // engine's fused modes otherwise (where they win or the dedicated kernels do not fit)
+    // Defaults: dedicated M-backward for O <= 128, rho-forward for O >= 96 and the
+    // small-O rho-forward for O <= 48 (from 8 trial pairs), the engine's fused modes
+    // otherwise (where they win or the dedicated kernels do not fit).  XT_W_KERNEL: 0 the
+    // engine, 1 the O >= 96 kernel, 3 the small-O kernel wherever they fit
     const char* em = getenv("XT_M_KERNEL");
     c->m_kernel = !(em && atoi(em) == 0);
     const char* ew = getenv("XT_W_KERNEL");
-    c->w_kernel = ew ? (atoi(ew) == 0 ? 0 : 1) : 2;
+    c->w_kernel = ew ? (atoi(ew) == 0 ? 0 : atoi(ew) == 3 ? 3 : 1) : 2;
   }
   *out = c;
   return 0;
@@ -1076,7 +1078,18 @@ static int xc_response(xt_ctx* c, int nz) {
       // the dedicated kernel pays off from ~6 occupied 16-row blocks up (O = 101: 168.6 vs
       // 173.1 ms/step; O = 34 / 37: 18 % / 15 % slower than the engine's mode 1)
       const bool w_ded = c->w_kernel == 1 || (c->w_kernel == 2 && O >= 96);
-      if (gga && w_ded && xc_rho_w_lds_bytes(O) <= 160 * 1024) {
+      const bool w_small = (c->w_kernel == 3 || (c->w_kernel == 2 && nzg >= 8)) &&
+                           xc_rho_ws_lds_bytes(O) <= 160 * 1024;
+      if (gga && w_small) {
+        // small-O kernel (xt_xcws.hip): every pair of a 64-point block, weights staged once
+        bool prof = false;
+        RET(prof_begin(c, 4, 2.0 * nzg * V * (double)n * (O + 3),
+                       8.0 * ((double)nzg * O * V + (double)n * O + 3.0 * n * V + 3.0 * n * nzg), &prof));
+        const int r = xc_rho_ws(O, nzg, V, n, PO, nmo, c->zp.p + gr[q].ch0 * chs, (long)nzg * V, V,
+                                PV + compP, compP, nmo, Rg[q], ldR[q], c->st);
+        if (r) return fail(r, "xc_rho_ws launch failed");
+        RET(prof_end(c, 4, prof));
+      } else if (gga && w_ded && xc_rho_w_lds_bytes(O) <= 160 * 1024) {
         // dedicated kernel (xt_xcw.hip); tag 4 timing
         bool prof = false;
         // flops: the T = PhiO^T Zp GEMM (2 O per T element) + the fused gradient

@@ -26,6 +26,20 @@ __device__ __forceinline__ double bld8(__amdgpu_buffer_rsrc_t r, unsigned voff, 
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
 
+// sum of v over the four 16-lane rows of a wave (lanes l, l^16, l^32, l^48), in every lane:
+// two row-pair swaps of both halves of the double (v_permlane16_swap, v_permlane32_swap)
+__device__ __forceinline__ double rows4(double v) {
+  auto pair = [](double x, bool p32) __attribute__((always_inline)) {
+    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+    const auto a = p32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                       : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = p32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                       : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+  };
+  return pair(pair(v, false), true);
+}
+
 // Fused XC grid contractions (GEMM modes, xt_gemm.hip).  Spin-channel x trial
 // vector pairs xg < nx, virtual index a < V, grid point g.
 //  mode 1 "rho forward":  rows m = 16 xg + a_l, reduce index r = a-block (a = 16 r + a_l),
@@ -138,6 +152,11 @@ int xc_back_m(int O, int nx, int V, int n, const double* PO, long ldp, const dou
 // PhiO[g][i] Zp[i zi + xg zx + a]; reads Zp up to 7 rows past O and WA - 1 columns past
 // V (zeroed slack), grid arrays XC_GRID_SLACK rows past n
 size_t xc_rho_w_lds_bytes(int O);
+// the same for O <= 48 (xt_xcws.hip): blocks of 64 points over every pair, gradient weights
+// staged once per 64-virtual chunk; same operand slack; XT_ERR_ARG past O = 48
+size_t xc_rho_ws_lds_bytes(int O);
+int xc_rho_ws(int O, int nx, int V, int n, const double* PO, long ldp, const double* Z, long zi, long zx,
+              const double* W, long wc, long wg, double* R, long rg, hipStream_t st);
 // Coulomb integrals over Cartesian Gaussians and AO values on the grid (xt_int.hip):
 // orbital l <= 3, total Hermite order 2 l_orb + l_ket <= kIntMaxL; AO values l <= kAoMaxL
 constexpr int kIntMaxLOrb = 3, kIntMaxL = 13, kAoMaxL = 4;

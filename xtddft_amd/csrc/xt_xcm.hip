@@ -66,19 +66,6 @@ struct BmLds {
   static constexpr int OA = 0, OW = 2 * A, OR = OW + 2 * W, ORM = OR + 2 * R, TOTAL = ORM + 2 * RM;
 };
 
-// rows4: sum of v over the four 16-lane rows (lanes l, l^16, l^32, l^48), in every lane
-__device__ __forceinline__ double rows4_m(double v) {
-  auto pair = [](double x, bool p32) XT_INLINE {
-    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-    const auto a = p32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
-                       : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-    const auto b = p32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
-                       : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-    return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
-  };
-  return pair(pair(v, false), true);
-}
-
 // RV > 0: the last 16-row block of the occupied rows holds only RV <= 8 rows (O = 16
 // (TM - 1) + RV); those rows are accumulated on the VALU (RV x 2 FMAs per k-step
 // against the same B fragments, ~55 cycles at RV = 5) instead of a 16-row MFMA
@@ -320,7 +307,7 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
     for (int r = 0; r < RV; ++r)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const double v = rows4_m(part[r][j]);
+        const double v = rows4(part[r][j]);
         const int i = 16 * TMM + r, a = a0 + 16 * j + r16;
         if (q == 0 && i < O && a < V) o[(long)i * ldo + (long)xg * V + a] = v;
       }

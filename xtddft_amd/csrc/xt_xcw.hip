@@ -60,19 +60,6 @@ constexpr int PP = 116;
 constexpr int RHO_W_MAX_O = 112;
 __host__ __device__ constexpr int rho_w_ki(int O) { return (O + 7) & ~7; }   // occupied rows (k-step pairs whole)
 
-// transposing 4-row sum (lanes l, l^16, l^32, l^48): every lane ends with the total
-__device__ __forceinline__ double rows4(double v) {
-  auto pair = [](double x, bool p32) XT_INLINE {
-    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-    const auto a = p32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
-                       : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-    const auto b = p32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
-                       : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-    return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
-  };
-  return pair(pair(v, false), true);
-}
-
 // PB trial pairs per block (8, 4, 2, 1; Davidson steps with few new vectors): the
 // H = 8 / PB waves of a pair split each a-tile's k-step pairs into H even ranges,
 // contract their partial T with the same staged weights (the contraction is linear in T)

@@ -1,0 +1,250 @@
+// XC rho-forward (W route) for small occupied spaces (O <= 48: C2, C5 and the small
+// molecules), the same contraction as xt_xcw.hip (XTDA.py:514, nr_uks_fxc):
+//
+//   rhoW[g][xg][c] = sum_a dPhiV_c[g][a] * sum_i PhiO[g][i] * Zp[i][xg][a]     (c < 3)
+//
+// At O = 37 an a-tile's K loop is 10 k-steps (80 MFMAs per wave), so the per-a-tile
+// costs of the O >= 96 kernel -- its barrier, the weight image staged per 8-pair set
+// and re-read from HBM by every one of the nx / 8 sets -- are 2.7x heavier relative to
+// the MFMAs there (0.41 of the FP64 roof at C5).  This kernel turns the loops around:
+//   * a block owns 64 grid points and ALL trial pairs: wave w walks pairs w, w + 8, ...;
+//   * the gradient weights dPhiV_c[g][a] of the block's points are staged into LDS once
+//     per 64-virtual chunk (one or two a-tiles), shared by every pair -- each weight is
+//     read from HBM once, and there is no barrier inside the pair loop;
+//   * PhiO (the MFMA B operand, K = i) is resident in LDS for the block's lifetime;
+//   * Zp (the A operand, rows = virtuals) streams global -> registers through a ring of
+//     2 KP slots: one whole a-tile of k-steps ahead, so every a-tile starts at slot 0
+//     and the walk over (chunk, pair, a-tile) prefetches across pairs and chunks;
+//   * the rows4 reduction of a pair's per-lane partials runs once per (pair, chunk); the
+//     chunks of one pair are summed in the output (the same lane reads back what it wrote
+//     a chunk earlier; the old value is prefetched when the pair starts).
+// Operand conventions are those of xc_rho_w (xt_internal.h): Zp readable 7 rows past O
+// and 31 columns past V (zeroed slack), PhiO / dPhiV rows past n are not read.
+#include <hip/hip_runtime.h>
+#include <mutex>
+#include <type_traits>
+#include "xt_internal.h"
+
+namespace xt {
+
+#define XT_INLINE __attribute__((always_inline))
+typedef double d4s __attribute__((ext_vector_type(4)));
+typedef double d2s __attribute__((ext_vector_type(2)));
+
+namespace {
+constexpr int SW_WA = 32;                  // virtuals per a-tile (2 MFMA row sub-tiles)
+constexpr int SW_TMA = SW_WA / 16;
+constexpr int SW_NW = 8;                   // waves per block
+constexpr int SW_TNG = 4;                  // 16-point column sub-tiles (64 grid points)
+constexpr int SW_GB = 16 * SW_TNG;
+constexpr int SW_AC = 2 * SW_WA;           // virtuals per staged chunk
+constexpr int SW_WP = SW_AC + 2;           // weight pitch, 2 mod 32: conflict-free ds_read_b64
+constexpr int SW_PP = 52;                  // PhiO pitch, 4 mod 8: conflict-free ds_read_b128
+constexpr int SW_W_IMG = 3 * SW_GB * SW_WP;
+constexpr size_t SW_LDS = sizeof(double) * ((size_t)SW_GB * SW_PP + SW_W_IMG);
+constexpr int SW_KP_MAX = 6;               // KI = 8 KP <= 48 <= SW_PP
+}  // namespace
+
+template <int KP>
+__global__ void __launch_bounds__(64 * SW_NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_xc_rho_ws(int O, int nx, int V, int n,
+            const double* __restrict__ PO, long ldp,
+            const double* __restrict__ Z, long zi, long zx,
+            const double* __restrict__ Wg, long wc, long wg,
+            double* __restrict__ Rout, long rg) {
+  constexpr int NT = 64 * SW_NW, KI = 8 * KP, ZD = 2 * KP;
+  constexpr int W_LD = 3 * SW_GB * SW_AC / NT;       // weight elements staged per thread and chunk (24)
+  static_assert(W_LD * NT == 3 * SW_GB * SW_AC && NT == 8 * SW_AC, "weight staging map");
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* sP = sm;                                   // [GB][PP]
+  double* sW = sm + SW_GB * SW_PP;                   // [3][GB][WP]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4, r16 = lane & 15;
+  const int g0 = blockIdx.x * SW_GB;
+  const int nat = (V + SW_WA - 1) / SW_WA;           // a-tiles
+  const int nck = (nat + 1) / 2;                     // chunks of two a-tiles
+  const int npw = wave < nx ? (nx - wave + SW_NW - 1) / SW_NW : 0;   // pairs of this wave
+
+  // ---- PhiO tile -> LDS, once (rows past O and points past n as zero) ---------------
+  for (int p = tid; p < KI * SW_GB; p += NT) {
+    const int g = p / KI, i = p % KI;
+    sP[g * SW_PP + i] = (i < O && g0 + g < n) ? PO[(long)(g0 + g) * ldp + i] : 0.0;
+  }
+
+  // ---- Zp walk: units (chunk, pair, a-tile of the chunk) in order; lane (q, r16) of
+  // k-step s supplies row i = 8 (s / 2) + 2 q + (s & 1) of virtual 16 t + r16 of the unit's
+  // a-tile.  zq[s] holds the current unit's k-step s until its MFMAs issue, then the next
+  // unit's (the last unit reloads itself: never consumed).
+  const __amdgpu_buffer_rsrc_t zrs = rsrc_of(Z);
+  const unsigned z_off = (unsigned)(((long)2 * q * zi + r16) * 8);
+  int wc_ = 0, wp_ = 0, wt_ = 0;                     // walker: chunk, pair index, tile in chunk
+  auto unit_off = [&](int ch, int pi, int tc) XT_INLINE {
+    return (int)((((long)(wave + SW_NW * pi)) * zx + (long)(2 * ch + tc) * SW_WA) * 8);
+  };
+  auto advance = [&]() XT_INLINE {                   // walker -> next unit (stays on the last)
+    const int ntc = 2 * wc_ + 1 < nat ? 2 : 1;
+    if (wt_ + 1 < ntc) { ++wt_; return; }
+    if (wp_ + 1 < npw) { ++wp_; wt_ = 0; return; }
+    if (wc_ + 1 < nck) { ++wc_; wp_ = 0; wt_ = 0; }
+  };
+  double zq[ZD][SW_TMA];
+  auto load_z = [&](int s, int uoff) XT_INLINE {     // s compile-time after unrolling
+    const int so = uoff + (8 * (s / 2) + (s & 1)) * (int)zi * 8;
+#pragma unroll
+    for (int t = 0; t < SW_TMA; ++t) zq[s][t] = bld8(zrs, z_off + 128 * t, so);
+  };
+  if (npw > 0) {
+    const int u0 = unit_off(0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < ZD; ++s) load_z(s, u0);
+    advance();
+  }
+
+  // B fragments of k-step pair p: columns 16 j + r16, rows 8 p + 2 q + {0, 1}
+  d2s bq[2][SW_TNG];
+  const double* const b_lane = sP + r16 * SW_PP + 2 * q;
+  auto bread = [&](int p, d2s* dst) XT_INLINE {
+    const d2s* src = (const d2s*)(b_lane + 8 * p);
+#pragma unroll
+    for (int j = 0; j < SW_TNG; ++j) dst[j] = src[(16 * j * SW_PP) / 2];
+  };
+
+  d4s acc[SW_TMA][SW_TNG];
+  double racc[SW_TNG][3];
+#pragma unroll
+  for (int j = 0; j < SW_TNG; ++j)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) racc[j][c] = 0.0;
+
+  // one a-tile (chunk-local tile tc) of the current unit: K loop, then the contraction
+  // racc[j][c] += sum_{t, r} T[a = 16 t + q + 4 r][g = 16 j + r16] * w_c[g][a]
+  auto tile = [&](int tc, int unext) XT_INLINE {
+#pragma unroll
+    for (int p = 0; p < KP; ++p) {
+      if (p + 1 < KP) bread(p + 1, bq[(p + 1) & 1]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int s = 2 * p + h;
+#pragma unroll
+        for (int t = 0; t < SW_TMA; ++t)
+#pragma unroll
+          for (int j = 0; j < SW_TNG; ++j)
+            acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(zq[s][t], bq[p & 1][j][h],
+                                                             s == 0 ? (d4s){0.0, 0.0, 0.0, 0.0} : acc[t][j], 0, 0, 0);
+        load_z(s, unext);
+      }
+    }
+    bread(0, bq[0]);                                 // the next tile's first pair (PhiO never changes)
+    const double* w = sW + r16 * SW_WP + tc * SW_WA + q;
+    constexpr int JH = SW_TNG / 2;
+    double wb[2][JH * 3];
+    auto wread = [&](int hh, double* dst) XT_INLINE {
+      const int rw_ = hh / 2, j0 = (hh % 2) * JH;
+      const int t = rw_ / 4, r = rw_ % 4;
+#pragma unroll
+      for (int jj = 0; jj < JH; ++jj)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) dst[3 * jj + c] = w[(c * SW_GB + 16 * (j0 + jj)) * SW_WP + 16 * t + 4 * r];
+    };
+    wread(0, wb[0]);
+#pragma unroll
+    for (int hh = 0; hh < 8 * SW_TMA; ++hh) {
+      if (hh + 1 < 8 * SW_TMA) wread(hh + 1, wb[(hh + 1) & 1]);
+      const int rw_ = hh / 2, j0 = (hh % 2) * JH;
+      const int t = rw_ / 4, r = rw_ % 4;
+#pragma unroll
+      for (int jj = 0; jj < JH; ++jj)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) racc[j0 + jj][c] += acc[t][j0 + jj][r] * wb[hh & 1][3 * jj + c];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // weight staging of chunk ch: thread element k -> plane k / 8, grid row wr + 8 (k % 8),
+  // column wa of the chunk (virtuals past V and points past n as zero)
+  const int wa = tid & (SW_AC - 1), wr = tid / SW_AC;
+  auto stage = [&](int ch) XT_INLINE {
+    const int a = ch * SW_AC + wa;
+    double rw[W_LD];
+#pragma unroll
+    for (int k = 0; k < W_LD; ++k) {
+      const int g = g0 + wr + 8 * (k % 8);
+      rw[k] = (a < V && g < n) ? Wg[(long)(k / 8) * wc + (long)g * wg + a] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < W_LD; ++k) sW[((k / 8) * SW_GB + wr + 8 * (k % 8)) * SW_WP + wa] = rw[k];
+  };
+
+  for (int ch = 0; ch < nck; ++ch) {
+    if (ch > 0) __syncthreads();                     // every wave is done with chunk ch - 1
+    stage(ch);
+    __syncthreads();
+    if (npw == 0) continue;
+    if (ch == 0) bread(0, bq[0]);
+    const int ntc = 2 * ch + 1 < nat ? 2 : 1;
+    for (int pi = 0; pi < npw; ++pi) {
+      const int xg = wave + SW_NW * pi;
+      // the chunks before this one left partial sums in the output: prefetch them, lane
+      // row q holding (and later storing) column sub-tile j = q
+      const int go = g0 + 16 * q + r16;
+      double prev[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) prev[c] = (ch > 0 && go < n) ? Rout[(long)go * rg + 3 * xg + c] : 0.0;
+      for (int tc = 0; tc < ntc; ++tc) {
+        const int un = unit_off(wc_, wp_, wt_);
+        advance();
+        tile(tc, un);
+      }
+      double tot[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+      for (int j = 0; j < SW_TNG; ++j)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const double v = rows4(racc[j][c]);      // the same total in every lane row
+          racc[j][c] = 0.0;
+          tot[c] = q == j ? v : tot[c];
+        }
+      if (go < n) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) Rout[(long)go * rg + 3 * xg + c] = prev[c] + tot[c];
+      }
+    }
+  }
+}
+
+size_t xc_rho_ws_lds_bytes(int O) { return (O + 7) / 8 <= SW_KP_MAX ? SW_LDS : (size_t)1 << 40; }
+
+int xc_rho_ws(int O, int nx, int V, int n, const double* PO, long ldp, const double* Z, long zi, long zx,
+              const double* W, long wc, long wg, double* R, long rg, hipStream_t st) {
+  if (O <= 0 || nx <= 0 || V <= 0 || n <= 0) return 0;
+  const int KP = (O + 7) / 8;
+  if (KP > SW_KP_MAX) return XT_ERR_ARG;
+  // 32-bit buffer offsets over Zp: KI rows (+ the a-tile overhang) of zi doubles
+  if ((double)(8 * KP + 1) * (double)zi * 8.0 >= 2147483647.0) return XT_ERR_ARG;
+  const int blocks = (n + SW_GB - 1) / SW_GB;
+  static std::mutex mu;
+  static unsigned long long done[SW_KP_MAX + 1] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+#define XT_WS(K)                                                                                           \
+  case K: {                                                                                                \
+    {                                                                                                      \
+      std::lock_guard<std::mutex> lk(mu);                                                                  \
+      if (dev >= 64 || !(done[K] >> dev & 1ull)) {                                                         \
+        (void)hipFuncSetAttribute((const void*)k_xc_rho_ws<K>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                  (int)SW_LDS);                                                            \
+        if (dev < 64) done[K] |= 1ull << dev;                                                              \
+      }                                                                                                    \
+    }                                                                                                      \
+    hipLaunchKernelGGL((k_xc_rho_ws<K>), dim3(blocks), dim3(64 * SW_NW), SW_LDS, st, O, nx, V, n, PO, ldp, Z, \
+                       zi, zx, W, wc, wg, R, rg);                                                          \
+    break;                                                                                                 \
+  }
+  switch (KP) { XT_WS(1) XT_WS(2) XT_WS(3) XT_WS(4) XT_WS(5) XT_WS(6) default: return XT_ERR_ARG; }
+#undef XT_WS
+  return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
+}
+
+}  // namespace xt
