@@ -29,6 +29,7 @@
 // slabs in a fixed order (deterministic), then applies alpha/beta.
 
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 #include <type_traits>
 #include <stdlib.h>
@@ -839,6 +840,11 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
   // The stored-exchange build's two-level rows (rdiv > 0) keep their measured tile (0.80 s
   // at the headline; 0.84 s on this one).
   if (ff && d.M >= 96 && d.N >= 96 && d.rdiv == 0) cfg = 9;
+  if (d.tag == 3) {   // tuning hook (A/B runs): XT_GEMM_L_CFG = 2, 3, 4, 5, 8 or 9 for XC back L
+    const char* e = getenv("XT_GEMM_L_CFG");
+    const int f = e ? atoi(e) : -1;
+    if (f == 2 || f == 3 || f == 4 || f == 5 || f == 8 || f == 9) cfg = f;
+  }
   const Cfg& c = kCfg[cfg];
   const long units = (long)p.R * ((d.K + c.bk - 1) / c.bk);
   int nsplit = choose_split(c, d.M, d.N, p.nbatch, units);
