@@ -840,6 +840,15 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
   // The stored-exchange build's two-level rows (rdiv > 0) keep their measured tile (0.80 s
   // at the headline; 0.84 s on this one).
   if (ff && d.M >= 96 && d.N >= 96 && d.rdiv == 0) cfg = 9;
+  // XC back L with few virtual columns: a 128-wide tile whose ragged column edge wastes much
+  // of the MFMA work (and stages whole panels for it) loses to the 64 x 64 tile (C2, N = V
+  // = 147: 2.45 -> 2.10 ms per step; 128 x 64: 2.15; C5, N = 117 in one 128-wide tile: 128 x
+  // 128 BK 32 stays, 2.88 against 3.22 / 3.31; C4 N = 661 and the headline N = 901 keep it
+  // too)
+  if (cfg == 9 && d.tag == 3) {
+    const double e128 = (double)d.N / (128.0 * ((d.N + 127) / 128)), e64 = (double)d.N / (64.0 * ((d.N + 63) / 64));
+    if (e128 < 0.75 && e64 - e128 > 0.12) cfg = 4;
+  }
   if (d.tag == 3) {   // tuning hook (A/B runs): XT_GEMM_L_CFG = 2, 3, 4, 5, 8 or 9 for XC back L
     const char* e = getenv("XT_GEMM_L_CFG");
     const int f = e ? atoi(e) : -1;

@@ -204,31 +204,33 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
         b[1][j] = w0[1] * g0[1] + w1[1] * g1[1] + w2[1] * g2[1];
       }
     };
-    d2m af[TMM > 0 ? TMM : 1], mr[RVA];
-    auto frag = [&](int p) XT_INLINE {          // pair p's A fragments and remainder values
+    // small O (TM <= 3: 8 MFMAs per k-step pair) reads pair p + 1's fragments during pair p:
+    // read in the pair that uses them, their LDS latency opened every pair with a stall
+    constexpr bool FA = TM <= 3;
+    d2m af[FA ? 2 : 1][TMM > 0 ? TMM : 1], mr[FA ? 2 : 1][RVA];
+    auto frag = [&](int p, int sl) XT_INLINE {  // pair p's A fragments and remainder values
 #pragma unroll
-      for (int t = 0; t < TMM; ++t) af[t] = sA[4 * p * PI + 16 * t];
+      for (int t = 0; t < TMM; ++t) af[sl][t] = sA[4 * p * PI + 16 * t];
       if constexpr (RV > 0) {
 #pragma unroll
-        for (int r = 0; r < RV; ++r) mr[r] = sM[4 * p * 8 + r];
+        for (int r = 0; r < RV; ++r) mr[sl][r] = sM[4 * p * 8 + r];
       }
     };
-    auto mma = [&](int p, double (*b)[2]) XT_INLINE {
-      (void)p;
+    auto mma = [&](double (*b)[2], int sl) XT_INLINE {
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         if constexpr (RV > 0) {
 #pragma unroll
           for (int r = 0; r < RV; ++r) {
-            part[r][0] += mr[r][st] * b[st][0];
-            part[r][1] += mr[r][st] * b[st][1];
+            part[r][0] += mr[sl][r][st] * b[st][0];
+            part[r][1] += mr[sl][r][st] * b[st][1];
           }
         }
 #pragma unroll
         for (int t = 0; t < TMM; ++t)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
-            acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t][st], b[st][j], acc[t][j], 0, 0, 0);
+            acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[sl][t][st], b[st][j], acc[t][j], 0, 0, 0);
       }
     };
     // Per k-step pair, one scheduling region: all its LDS reads first (pair p's fragments,
@@ -239,12 +241,17 @@ k_xc_back_m(int O, int nx, int V, int n, int ktiles_per_split,
     constexpr int NMF = 2 * 2 * (TMM > 0 ? TMM : 1);
     double b[2][2][2];
     gen(0, b[0]);
+    if constexpr (FA) frag(0, 0);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int p = 0; p < KP; ++p) {
-      frag(p);
+      if constexpr (FA) {
+        if (p + 1 < KP) frag(p + 1, (p + 1) & 1);
+      } else {
+        frag(p, 0);
+      }
       if (p + 1 < KP) gen(p + 1, b[(p + 1) & 1]);
-      mma(p, b[p & 1]);
+      mma(b[p & 1], FA ? (p & 1) : 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);   // the first fragments
 #pragma unroll
       for (int k = 0; k < NMF / 4; ++k) {

@@ -42,17 +42,20 @@ constexpr int SW_WP = SW_AC + 2;           // weight pitch, 2 mod 32: conflict-f
 constexpr int SW_PP = 52;                  // PhiO pitch, 4 mod 8: conflict-free ds_read_b128
 constexpr int SW_W_IMG = 3 * SW_GB * SW_WP;
 constexpr size_t SW_LDS = sizeof(double) * ((size_t)SW_GB * SW_PP + SW_W_IMG);
-constexpr int SW_KP_MAX = 6;               // KI = 8 KP <= 48 <= SW_PP
+constexpr int SW_KS_MAX = 12;              // k-steps: KI = 4 KS <= 48 <= SW_PP
 }  // namespace
 
-template <int KP>
+// KS = ceil(O / 4) k-steps per a-tile: KS / 2 k-step pairs (one ds_read_b128 of PhiO per
+// pair) and, for odd KS, one single k-step (O = 34: 9 k-steps instead of 10)
+template <int KS>
 __global__ void __launch_bounds__(64 * SW_NW) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_xc_rho_ws(int O, int nx, int V, int n,
             const double* __restrict__ PO, long ldp,
             const double* __restrict__ Z, long zi, long zx,
             const double* __restrict__ Wg, long wc, long wg,
             double* __restrict__ Rout, long rg) {
-  constexpr int NT = 64 * SW_NW, KI = 8 * KP, ZD = 2 * KP;
+  constexpr int NT = 64 * SW_NW, KP = KS / 2, KI = 4 * KS, ZD = KS;
+  constexpr bool ODD = (KS & 1) != 0;
   constexpr int W_LD = 3 * SW_GB * SW_AC / NT;       // weight elements staged per thread and chunk (24)
   static_assert(W_LD * NT == 3 * SW_GB * SW_AC && NT == 8 * SW_AC, "weight staging map");
   extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -74,11 +77,12 @@ k_xc_rho_ws(int O, int nx, int V, int n,
   }
 
   // ---- Zp walk: units (chunk, pair, a-tile of the chunk) in order; lane (q, r16) of
-  // k-step s supplies row i = 8 (s / 2) + 2 q + (s & 1) of virtual 16 t + r16 of the unit's
-  // a-tile.  zq[s] holds the current unit's k-step s until its MFMAs issue, then the next
+  // k-step s supplies row i = 8 (s / 2) + 2 q + (s & 1) (the single step: 8 KP + q) of
+  // virtual 16 t + r16 of the unit's a-tile.  zq[s] holds the current unit's k-step s until its MFMAs issue, then the next
   // unit's (the last unit reloads itself: never consumed).
   const __amdgpu_buffer_rsrc_t zrs = rsrc_of(Z);
   const unsigned z_off = (unsigned)(((long)2 * q * zi + r16) * 8);
+  const unsigned z_off1 = (unsigned)(((long)q * zi + r16) * 8);
   int wc_ = 0, wp_ = 0, wt_ = 0;                     // walker: chunk, pair index, tile in chunk
   auto unit_off = [&](int ch, int pi, int tc) XT_INLINE {
     return (int)((((long)(wave + SW_NW * pi)) * zx + (long)(2 * ch + tc) * SW_WA) * 8);
@@ -91,9 +95,10 @@ k_xc_rho_ws(int O, int nx, int V, int n,
   };
   double zq[ZD][SW_TMA];
   auto load_z = [&](int s, int uoff) XT_INLINE {     // s compile-time after unrolling
-    const int so = uoff + (8 * (s / 2) + (s & 1)) * (int)zi * 8;
+    const bool single = ODD && s == KS - 1;
+    const int so = uoff + (single ? 8 * KP : 8 * (s / 2) + (s & 1)) * (int)zi * 8;
 #pragma unroll
-    for (int t = 0; t < SW_TMA; ++t) zq[s][t] = bld8(zrs, z_off + 128 * t, so);
+    for (int t = 0; t < SW_TMA; ++t) zq[s][t] = bld8(zrs, (single ? z_off1 : z_off) + 128 * t, so);
   };
   if (npw > 0) {
     const int u0 = unit_off(0, 0, 0);
@@ -102,13 +107,24 @@ k_xc_rho_ws(int O, int nx, int V, int n,
     advance();
   }
 
-  // B fragments of k-step pair p: columns 16 j + r16, rows 8 p + 2 q + {0, 1}
+  // B fragments of k-step pair p: columns 16 j + r16, rows 8 p + 2 q + {0, 1}; of the
+  // single k-step: rows 8 KP + q
   d2s bq[2][SW_TNG];
+  double bs[SW_TNG];
   const double* const b_lane = sP + r16 * SW_PP + 2 * q;
   auto bread = [&](int p, d2s* dst) XT_INLINE {
     const d2s* src = (const d2s*)(b_lane + 8 * p);
 #pragma unroll
     for (int j = 0; j < SW_TNG; ++j) dst[j] = src[(16 * j * SW_PP) / 2];
+  };
+  auto bread1 = [&]() XT_INLINE {
+    const double* src = sP + r16 * SW_PP + 8 * KP + q;
+#pragma unroll
+    for (int j = 0; j < SW_TNG; ++j) bs[j] = src[16 * j * SW_PP];
+  };
+  auto bfirst = [&]() XT_INLINE {                   // the B operand of a tile's first k-step
+    if constexpr (KP > 0) bread(0, bq[0]);
+    else bread1();
   };
 
   d4s acc[SW_TMA][SW_TNG];
@@ -124,6 +140,7 @@ k_xc_rho_ws(int O, int nx, int V, int n,
 #pragma unroll
     for (int p = 0; p < KP; ++p) {
       if (p + 1 < KP) bread(p + 1, bq[(p + 1) & 1]);
+      else if constexpr (ODD) bread1();
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int s = 2 * p + h;
@@ -136,7 +153,16 @@ k_xc_rho_ws(int O, int nx, int V, int n,
         load_z(s, unext);
       }
     }
-    bread(0, bq[0]);                                 // the next tile's first pair (PhiO never changes)
+    if constexpr (ODD) {
+#pragma unroll
+      for (int t = 0; t < SW_TMA; ++t)
+#pragma unroll
+        for (int j = 0; j < SW_TNG; ++j)
+          acc[t][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(zq[KS - 1][t], bs[j],
+                                                           KS == 1 ? (d4s){0.0, 0.0, 0.0, 0.0} : acc[t][j], 0, 0, 0);
+      load_z(KS - 1, unext);
+    }
+    bfirst();                                        // the next tile's first k-step (PhiO never changes)
     const double* w = sW + r16 * SW_WP + tc * SW_WA + q;
     constexpr int JH = SW_TNG / 2;
     double wb[2][JH * 3];
@@ -182,7 +208,7 @@ k_xc_rho_ws(int O, int nx, int V, int n,
     stage(ch);
     __syncthreads();
     if (npw == 0) continue;
-    if (ch == 0) bread(0, bq[0]);
+    if (ch == 0) bfirst();
     const int ntc = 2 * ch + 1 < nat ? 2 : 1;
     for (int pi = 0; pi < npw; ++pi) {
       const int xg = wave + SW_NW * pi;
@@ -214,18 +240,18 @@ k_xc_rho_ws(int O, int nx, int V, int n,
   }
 }
 
-size_t xc_rho_ws_lds_bytes(int O) { return (O + 7) / 8 <= SW_KP_MAX ? SW_LDS : (size_t)1 << 40; }
+size_t xc_rho_ws_lds_bytes(int O) { return (O + 3) / 4 <= SW_KS_MAX ? SW_LDS : (size_t)1 << 40; }
 
 int xc_rho_ws(int O, int nx, int V, int n, const double* PO, long ldp, const double* Z, long zi, long zx,
               const double* W, long wc, long wg, double* R, long rg, hipStream_t st) {
   if (O <= 0 || nx <= 0 || V <= 0 || n <= 0) return 0;
-  const int KP = (O + 7) / 8;
-  if (KP > SW_KP_MAX) return XT_ERR_ARG;
+  const int KS = (O + 3) / 4;
+  if (KS > SW_KS_MAX) return XT_ERR_ARG;
   // 32-bit buffer offsets over Zp: KI rows (+ the a-tile overhang) of zi doubles
-  if ((double)(8 * KP + 1) * (double)zi * 8.0 >= 2147483647.0) return XT_ERR_ARG;
+  if ((double)(4 * KS + 1) * (double)zi * 8.0 >= 2147483647.0) return XT_ERR_ARG;
   const int blocks = (n + SW_GB - 1) / SW_GB;
   static std::mutex mu;
-  static unsigned long long done[SW_KP_MAX + 1] = {};
+  static unsigned long long done[SW_KS_MAX + 1] = {};
   int dev = 0;
   (void)hipGetDevice(&dev);
 #define XT_WS(K)                                                                                           \
@@ -242,7 +268,10 @@ int xc_rho_ws(int O, int nx, int V, int n, const double* PO, long ldp, const dou
                        zi, zx, W, wc, wg, R, rg);                                                          \
     break;                                                                                                 \
   }
-  switch (KP) { XT_WS(1) XT_WS(2) XT_WS(3) XT_WS(4) XT_WS(5) XT_WS(6) default: return XT_ERR_ARG; }
+  switch (KS) {
+    XT_WS(1) XT_WS(2) XT_WS(3) XT_WS(4) XT_WS(5) XT_WS(6) XT_WS(7) XT_WS(8) XT_WS(9) XT_WS(10) XT_WS(11) XT_WS(12)
+    default: return XT_ERR_ARG;
+  }
 #undef XT_WS
   return hipGetLastError() == hipSuccess ? 0 : XT_ERR_HIP;
 }
