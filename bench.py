@@ -51,9 +51,8 @@ sys.path.insert(0, ROOT)
 FP64_PEAK_TFLOPS = 78.6     # MI355X dense FP64 matrix peak (AMD spec); 74.2 measured (tools/mfma_probe.hip)
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8.0 TB/s spec
 # the newest committed rocprofv3 FETCH / WRITE summary (tools/parse_prof.py)
-PMC_SUMMARY = next((os.path.join(ROOT, "profiles", f"r0{k}_pmc_summary.json") for k in (5, 4)
-                    if os.path.exists(os.path.join(ROOT, "profiles", f"r0{k}_pmc_summary.json"))),
-                   os.path.join(ROOT, "profiles", "r04_pmc_summary.json"))
+# committed rocprofv3 PMC summaries, newest round first
+PMC_SUMMARIES = [os.path.join(ROOT, "profiles", f"r0{k}_pmc_summary.json") for k in (5, 4)]
 
 KIND_NAME = {"XTDA": "X-TDA", "SF_UP": "SF-TDA (spin-flip up)", "SF_DOWN": "SF-TDA (spin-flip down)",
              "XSF": "XSF-TDA"}
@@ -472,14 +471,18 @@ def converge(args, w, allreduce):
 
 # ---------------------------------------------------------------------------
 def load_traffic(config, tag_name):
-    """HBM bytes per launch of the tagged kernel from this config's committed
-    rocprofv3 PMC summary (the newest profiles/r0*_pmc_summary.json), None if absent."""
-    try:
-        with open(PMC_SUMMARY) as f:
-            d = json.load(f)
-        return d.get(config, {}).get(tag_name, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        return None
+    """HBM bytes per launch of the tagged kernel from the newest committed rocprofv3 PMC
+    summary (profiles/r0*_pmc_summary.json) that holds this config and class, None if none."""
+    for path in PMC_SUMMARIES:
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        v = d.get(config, {}).get(tag_name, {}).get("hbm_bytes_per_launch")
+        if v is not None:
+            return v
+    return None
 
 
 def roofline_of(args, stats_acc, steps, world=1):
