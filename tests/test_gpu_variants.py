@@ -4,13 +4,13 @@ its 160-row streaming tile and its batching.
 
 Automatic selection (xt_ctx.hip): the dedicated M-backward kernel (xt_xcm.hip) for
 O <= 128 and the generic engine's fused mode 2 above; the dedicated rho-forward
-kernel (xt_xcw.hip) for O >= 96, the small-O rho-forward kernel (xt_xcws.hip) for
+kernel (xt_xcw.hip) for O > 64, the small-O rho-forward kernel (xt_xcws.hip) for
 O <= 48 from 8 trial pairs, and the engine's fused mode 1 in between.
 The two test hooks (environment, read once at xt_create) force either side outside
 its automatic range so each path is checked at every occupied-row shape:
 
 * XT_M_KERNEL=0 -> XC M-backward through the engine's mode 2
-* XT_W_KERNEL=0 / 1 / 3 -> XC rho-forward through the engine's mode 1 / the O >= 96
+* XT_W_KERNEL=0 / 1 / 3 -> XC rho-forward through the engine's mode 1 / the O > 64
   kernel / the small-O kernel (every pair count; O <= 48)
 
 Tolerance: 1e-12 relative max-norm on sigma (FP64 round-off of a different

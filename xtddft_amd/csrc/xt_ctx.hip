@@ -251,10 +251,10 @@ int xt_create(const xt_desc* desc, xt_ctx** out) {
   {
     // the only environment knobs, read here once per context: which XC kernels run the
     // fused classes outside their automatic ranges (tests/test_gpu_variants.py).
-    // Defaults: dedicated M-backward for O <= 128, rho-forward for O >= 96 and the
+    // Defaults: dedicated M-backward for O <= 128, rho-forward for O > 64 and the
     // small-O rho-forward for O <= 48 (from 8 trial pairs), the engine's fused modes
     // otherwise (where they win or the dedicated kernels do not fit).  XT_W_KERNEL: 0 the
-    // engine, 1 the O >= 96 kernel, 3 the small-O kernel wherever they fit
+    // engine, 1 the O > 64 kernel, 3 the small-O kernel wherever they fit
     const char* em = getenv("XT_M_KERNEL");
     c->m_kernel = !(em && atoi(em) == 0);
     const char* ew = getenv("XT_W_KERNEL");
@@ -1075,9 +1075,10 @@ static int xc_response(xt_ctx* c, int nz) {
           RET(gemm(c, ft));
         }
       }
-      // the dedicated kernel pays off from ~6 occupied 16-row blocks up (O = 101: 168.6 vs
-      // 173.1 ms/step; O = 34 / 37: 18 % / 15 % slower than the engine's mode 1)
-      const bool w_ded = c->w_kernel == 1 || (c->w_kernel == 2 && O >= 96);
+      // the dedicated kernel pays off from ~5 occupied 16-row blocks up (O = 101: 168.6 vs
+      // 173.1 ms/step; O = 91, C3mc: 75.2 vs 87.0; O = 34 / 37: 18 % / 15 % slower than the
+      // engine's mode 1, and the small-O kernel takes O <= 48)
+      const bool w_ded = c->w_kernel == 1 || (c->w_kernel == 2 && O > 64);
       const bool w_small = (c->w_kernel == 3 || (c->w_kernel == 2 && nzg >= 8)) &&
                            xc_rho_ws_lds_bytes(O) <= 160 * 1024;
       if (gga && w_small) {

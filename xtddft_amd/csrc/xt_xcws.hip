@@ -4,7 +4,7 @@
 //   rhoW[g][xg][c] = sum_a dPhiV_c[g][a] * sum_i PhiO[g][i] * Zp[i][xg][a]     (c < 3)
 //
 // At O = 37 an a-tile's K loop is 10 k-steps (80 MFMAs per wave), so the per-a-tile
-// costs of the O >= 96 kernel -- its barrier, the weight image staged per 8-pair set
+// costs of the large-O kernel (xt_xcw.hip) -- its barrier, the weight image staged per 8-pair set
 // and re-read from HBM by every one of the nx / 8 sets -- are 2.7x heavier relative to
 // the MFMAs there (0.41 of the FP64 roof at C5).  This kernel turns the loops around:
 //   * a block owns 64 grid points and ALL trial pairs: wave w walks pairs w, w + 8, ...;
