@@ -198,3 +198,22 @@ def test_device_mf_shards_concatenate_to_the_unsharded_tensors():
         assert torch.equal(torch.cat([p.fxc for p in parts], -1), full.fxc)
         assert torch.equal(torch.cat([p.fxc_sf_mc for p in parts], -1), full.fxc_sf_mc)
         assert torch.equal(make_device_mf(shard=(1, n), full_aux=True, **kw).cderi, full.cderi)
+
+
+def test_nlc_functional_follows_the_reference():
+    """VV10 (NLC): the reference adds get_vnlc_resp in the X-TDA Davidson response only
+    (XTDA.py:515-517) -- not built here, so that path refuses instead of silently differing;
+    the explicit A and the SF / XSF paths leave it out with the reference's warning
+    (XTDA.py:166-169, SF_TDA.py:490-493, 869-872)."""
+    from xtddft_amd.sf_tda import SF_TDA_up
+    from xtddft_amd.synthetic import make_mf
+    from xtddft_amd.xsf_tda import XSF_TDA
+    from xtddft_amd.xtda import XTDA
+    mf = make_mf(nao=20, nc=4, no=2, ngrid=500, xctype="GGA", hyb=0.2)
+    mf.nlc = True
+    with pytest.raises(NotImplementedError, match="get_vnlc_resp"):
+        XTDA(None, mf).kernel()
+    with pytest.warns(RuntimeWarning, match="NLC functional"):
+        SF_TDA_up(mf)
+    with pytest.warns(RuntimeWarning, match="NLC functional"):
+        XSF_TDA(mf)

@@ -111,6 +111,7 @@ class MeanField:
     fxc: Optional[np.ndarray] = None
     fxc_sf: Optional[np.ndarray] = None
     fxc_sf_mc: Optional[np.ndarray] = None
+    nlc: bool = False          # the SCF functional carries a VV10 non-local term (mf.do_nlc())
     cderi_lr: Optional[np.ndarray] = None
     xc: str = "synthetic"
     xctype: str = "GGA"

@@ -25,7 +25,7 @@ from . import davidson as _dav
 from .meanfield import MeanField
 from .operator import DeviceOperator
 from .parallel import require_group
-from .utils import order_sf_down
+from .utils import nlc_check, order_sf_down
 
 HA2EV = 27.2113834   # SF_TDA.py:15
 
@@ -159,6 +159,7 @@ class _SFBase:
         self.device = device
         self.shard = tuple(shard)
         require_group(self.shard[1])
+        nlc_check(mf)
         self.nc, self.no, self.nv = _sf_shape(mf)
 
     def get_Amat(self):

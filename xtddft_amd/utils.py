@@ -59,3 +59,23 @@ def st2so(eigvec, nc, no, nv):
     co0 = eigvec[(nc + no) * nv:(nc + no) * nv + no * nc]
     cv1 = eigvec[(nc + no) * nv + no * nc:]
     return np.concatenate(((cv0 + cv1) / np.sqrt(2), ov0, co0, (cv0 - cv1) / np.sqrt(2)), axis=0)
+
+
+NLC_SF_WARNING = ('NLC functional found in DFT object.  Its second derivative is not available. '
+                  'Its contribution is not included in the response function.')
+
+
+def nlc_check(mf, davidson_xtda=False):
+    """The reference's treatment of a VV10 (NLC) functional: the X-TDA / U-TDA Davidson
+    response adds ``get_vnlc_resp`` (XTDA.py:515-517), which is not built here, so that path
+    refuses; every other path (explicit X-TDA A, XTDA.py:166-169; SF-TDA, SF_TDA.py:490-493,
+    669-672, 869-872; XSF-TDA through the same kernels) leaves it out with this warning."""
+    if not getattr(mf, "nlc", False):
+        return
+    if davidson_xtda:
+        raise NotImplementedError("the VV10 (NLC) response term of the X-TDA Davidson path "
+                                  "(XTDA.py:515-517, pyscf.hessian.rks.get_vnlc_resp) is not built; "
+                                  "use_Davidson=False runs the explicit A, which leaves it out as the "
+                                  "reference does")
+    import warnings
+    warnings.warn(NLC_SF_WARNING, RuntimeWarning, stacklevel=3)

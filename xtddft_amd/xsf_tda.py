@@ -33,7 +33,7 @@ from . import davidson as _dav
 from .meanfield import MeanField
 from .parallel import require_group
 from .sf_tda import _check_method, _dense, mf_info, sf_operator
-from .utils import HA2EV_XSF
+from .utils import HA2EV_XSF, nlc_check
 
 
 def get_vect(no):
@@ -92,6 +92,7 @@ class XSF_TDA:
         self.device = device
         self.shard = tuple(shard)
         require_group(self.shard[1])
+        nlc_check(mf)
         info = mf.shape_info()
         self.nc, self.no, self.nv = info['nc'], info['no'], info['nv']
         self.nocc_a, self.nocc_b = info['nocc_a'], info['nocc_b']

@@ -20,7 +20,7 @@ from . import davidson as _dav
 from .meanfield import MeanField
 from .operator import DeviceOperator
 from .parallel import require_group
-from .utils import HA2EV, EVXNM, order_pyscf2my, so2st as _so2st
+from .utils import HA2EV, EVXNM, nlc_check, order_pyscf2my, so2st as _so2st
 
 CGS2AU = 1 / (235.7220 * 2)    # xtddft/utils/unit.py:9 (rotatory strength a.u. -> cgs)
 
@@ -57,6 +57,7 @@ class XTDA:
             raise NotImplementedError("tensor-basis X_TDA (XTDA.py:947-1483) is outside the hot path")
         if self.basis != 'orbital':
             raise ValueError('basis must be tensor or orbital')
+        nlc_check(self.mf, davidson_xtda=self.use_Davidson)
         if self.use_Davidson:
             return self.Davidson()
         return self.full_diag()
