@@ -51,12 +51,12 @@ def env():
 
 @pytest.mark.parametrize("knobs", [dict(), dict(XT_M_KERNEL=0), dict(XT_W_KERNEL=0), dict(XT_M_KERNEL=0, XT_W_KERNEL=0),
                                    dict(XT_M_KERNEL=1, XT_W_KERNEL=1), dict(XT_W_KERNEL=3)])
-@pytest.mark.parametrize("nc,no,nao", [(2, 1, 20), (9, 2, 40), (5, 2, 26), (33, 1, 60), (35, 2, 70), (95, 2, 130),
-                                      (99, 2, 140), (120, 3, 150)])
+@pytest.mark.parametrize("nc,no,nao", [(2, 1, 20), (9, 2, 40), (5, 2, 26), (33, 1, 60), (35, 2, 70), (40, 1, 72),
+                                      (45, 2, 80), (95, 2, 130), (99, 2, 140), (120, 3, 150)])
 def test_xc_kernel_variants(hiplib, env, knobs, nc, no, nao):
-    """O = 3, 11, 7, 34, 37, 97, 101 and 123: one to eight 16-row sub-tiles of the dedicated
-    kernels, with (34, 37, 97, 101) and without a VALU remainder-row block; the small-O
-    rho-forward with 1, 3, 9 (odd: one single k-step) and 2, 10 k-steps."""
+    """O = 3, 11, 7, 34, 37, 41, 47, 97, 101 and 123: one to eight 16-row sub-tiles of the
+    dedicated kernels, with (34, 37, 41, 47, 97, 101) and without a VALU remainder-row block;
+    the small-O rho-forward with 1, 3, 9, 11 (odd: one single k-step) and 2, 10, 12 k-steps."""
     from xtddft_amd.operator import DeviceOperator
     env(**knobs)
     mf = make_mf(nao=nao, nc=nc, no=no, ngrid=3000, xctype="GGA", hyb=0.2)
