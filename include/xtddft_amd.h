@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define XT_ABI_VERSION 6
+#define XT_ABI_VERSION 7
 
 #define XT_PTR_HOST 0
 #define XT_PTR_DEVICE 1
@@ -141,6 +141,14 @@ int xt_set_exchange_mode(xt_ctx* ctx, int mode, double max_gib);
    xt_naux reports the window; re-partitioning or a stored-exchange rebuild needs
    the factor set again. */
 int xt_prepare(xt_ctx* ctx, int* k_mode, double* k_gib);
+/* What XT_K_AUTO resolves to on this context (*stored = 1 / 0) and the stored
+   matrix's footprint (GiB), without building anything.  The resolution depends
+   on this GPU's free HBM, so the ranks of a partitioned operator must agree
+   before they build: a rank that streams its stored ROWS and a rank that
+   contracts its aux WINDOW directly do not sum to the operator.  The host side
+   takes the minimum over ranks and sets the mode explicitly
+   (xtddft_amd/operator.py).  Same fit rule as xt_prepare. */
+int xt_exchange_plan(xt_ctx* ctx, int* stored, double* k_gib);
 
 /* Rank partition of a sharded operator (one process per GPU):
    the context keeps the whole MO factor but contracts J, the direct exchange

@@ -99,7 +99,7 @@ def _worker_lockstep(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import xtda as oxtda
-    from xtddft_amd.parallel import LockstepError, allreduce_sigma, lockstep_check
+    from xtddft_amd.parallel import LockstepError, agree_min, allreduce_sigma, lockstep_check
     from xtddft_amd.synthetic import make_trial_vectors
     out = {}
     # (a) the shards of the block-seeded generator: partial sigma all-reduced == 1-rank operator
@@ -119,6 +119,8 @@ def _worker_lockstep(rank, world, port, q):
         out["raised"] = False
     except LockstepError:
         out["raised"] = True
+    # (c) a rank-local resolution made collectively: the stored exchange only if every rank fits
+    out["agree"] = (agree_min(1 if rank == 0 else 0), agree_min(1))
     q.put((rank, out))
     dist.destroy_process_group()
 
@@ -127,7 +129,9 @@ def test_block_seeded_shards_and_lockstep_guard():
     """World 2 over gloo: (a) bench's synthetic mean field generated per rank from global
     block seeds sums (partial sigma, all-reduced) to the 1-rank operator, so a sharded run
     solves the N = 1 problem; (b) ``lockstep_check`` passes identical decision data and
-    raises LockstepError on EVERY rank when one rank's data differ (no rank left waiting)."""
+    raises LockstepError on EVERY rank when one rank's data differ (no rank left waiting);
+    (c) ``agree_min`` gives every rank the same exchange-mode decision (DeviceOperator: the
+    stored exchange only when it fits on every rank)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -140,3 +144,4 @@ def test_block_seeded_shards_and_lockstep_guard():
         assert pr.exitcode == 0
     assert res[0]["shard_err"] < 1e-13
     assert res[0]["raised"] and res[1]["raised"]
+    assert res[0]["agree"] == res[1]["agree"] == (0, 1)

@@ -28,7 +28,7 @@ def test_library_builds_and_exports_every_header_symbol(hiplib):
     for s in syms:
         assert hasattr(hiplib, s), s
     from xtddft_amd._capi import ABI_VERSION
-    assert hiplib.xt_abi_version() == ABI_VERSION == 6
+    assert hiplib.xt_abi_version() == ABI_VERSION == 7
 
 
 def test_desc_layout_matches_c_header(tmp_path):

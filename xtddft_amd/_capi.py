@@ -28,7 +28,7 @@ EXPORTS = [
     "xt_set_orbitals", "xt_set_fock_mo", "xt_set_orbital_energies", "xt_set_jk_df",
     "xt_set_jk_eri8", "xt_naux",
     "xt_set_grid", "xt_set_oo_basis", "xt_apply", "xt_dim", "xt_last_timings",
-    "xt_xsf_j_diagonals", "xt_set_exchange_mode", "xt_prepare", "xt_set_partition", "xt_set_profile",
+    "xt_xsf_j_diagonals", "xt_set_exchange_mode", "xt_prepare", "xt_exchange_plan", "xt_set_partition", "xt_set_profile",
     "xt_profile_stats", "xt_profile_bytes", "xt_dgemm", "xt_dgemm_strided", "xt_precond", "xt_row_norms2", "xt_row_scale", "xt_build_id",
     "xt_int3c2e_cart", "xt_int2e_cart", "xt_eval_ao",
 ]
@@ -44,7 +44,7 @@ class XtDesc(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 6   # include/xtddft_amd.h XT_ABI_VERSION
+ABI_VERSION = 7   # include/xtddft_amd.h XT_ABI_VERSION
 
 
 class LibraryMissing(RuntimeError):
@@ -93,6 +93,7 @@ def lib():
     L.xt_xsf_j_diagonals.argtypes = [vp, dp, dp, c_int]
     L.xt_set_exchange_mode.argtypes = [vp, c_int, c_double]
     L.xt_prepare.argtypes = [vp, POINTER(c_int), POINTER(c_double)]
+    L.xt_exchange_plan.argtypes = [vp, POINTER(c_int), POINTER(c_double)]
     L.xt_set_partition.argtypes = [vp, c_int, c_int, c_int, c_int]
     L.xt_set_profile.argtypes = [vp, c_int]
     L.xt_profile_stats.argtypes = [vp, c_int, dp]

@@ -977,6 +977,15 @@ extern "C" int xt_set_exchange_mode(xt_ctx* c, int mode, double max_gib) {
   return 0;
 }
 
+extern "C" int xt_exchange_plan(xt_ctx* c, int* stored, double* k_gib) {
+  if (!c) return fail(XT_ERR_ARG, "null ctx");
+  (void)hipSetDevice(c->d.device);
+  RET(resolve_kmode(c));
+  if (stored) *stored = c->k_resolved == 1 ? 1 : 0;
+  if (k_gib) *k_gib = kx_doubles(c) * 8.0 / (double)((size_t)1 << 30);
+  return 0;
+}
+
 // Once a partitioned context holds its rows of the stored exchange, only the aux window
 // [win_p0, win_p0 + win_np) of the MO factor is ever read again (J, the XSF Delta-A, the
 // preconditioner diagonals): the other rows are dropped, so a replicated factor costs

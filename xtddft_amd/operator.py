@@ -140,6 +140,16 @@ class DeviceOperator:
             self._set_partition(kind, nc, no)
         _capi.check(L.xt_set_exchange_mode(h, _capi.K_MODE[k_mode], float(k_max_gib)),
                     "xt_set_exchange_mode")
+        if self.replicate_df and k_mode == "auto":
+            # the auto rule reads this GPU's free HBM: the ranks agree (store only if every
+            # rank's rows fit) before anything is built -- stored rows on one rank and a
+            # direct aux window on another do not sum to the operator
+            fits, gib = ctypes.c_int(), ctypes.c_double()
+            _capi.check(L.xt_exchange_plan(h, ctypes.byref(fits), ctypes.byref(gib)), "xt_exchange_plan")
+            from .parallel import agree_min
+            k_mode = "stored" if agree_min(fits.value) else "direct"
+            _capi.check(L.xt_set_exchange_mode(h, _capi.K_MODE[k_mode], float(k_max_gib)),
+                        "xt_set_exchange_mode")
         self.prepare()
         self.setup_s["prepare"] = self.prepare_s
 
