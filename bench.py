@@ -554,7 +554,8 @@ def breakdown(op, z, out, allreduce, sync, stats_acc, steps, rank, world, reps=2
         ta += t1 - t0
         tr += time.perf_counter() - t1
     return dict(rank=rank, ax_ms=round(1e3 * ta / reps, 3), allreduce_ms=round(1e3 * tr / reps, 3),
-                sigma_mb=round(out.numel() * 8 / 1e6, 3),
+                sigma_mb=round(out.numel() * 8 / 1e6, 3), k_mode=getattr(op, "k_mode", None),
+                partition=getattr(op, "partition", None),
                 kernel_ms={k: round(v["ms"] / steps, 3) for k, v in stats_acc.items() if v["launches"]})
 
 
