@@ -83,7 +83,10 @@ class DeviceOperator:
         k_mode: exchange evaluation ('auto' | 'direct' | 'stored', see
         xt_set_exchange_mode); k_max_gib caps the stored matrix in auto mode.
         replicate_df: keep the whole factor on every rank and partition by aux
-        window + exchange rows (default: k_mode != 'direct')."""
+        window + exchange rows (default: k_mode != 'direct').  With replicate_df, k_mode
+        'auto' and an initialised process group, construction is a collective: the ranks
+        agree on stored vs direct exchange (the minimum of their fits), so every rank of
+        the group must construct its operator."""
         L = _capi.lib()
         self.mf, self.kind = mf, kind
         if sf_kernel not in _capi.SF_KERNEL:
