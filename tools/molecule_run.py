@@ -2,6 +2,7 @@
 
     python tools/molecule_run.py --molecule naphthalene+ [--nroots 20] [--out FILE]
     python tools/molecule_run.py --molecule ch2
+    python tools/molecule_run.py --molecule naphthalene+ --kind xsf [--sa 0]
 
 * naphthalene+ : C10H8+ doublet, cc-pVDZ (180 AOs: the nao of BASELINE config C2's
   def2-SVP), ROKS B3LYP (the reference's default functional, XTDA.py:1526), X-TDA 20 roots;
@@ -13,6 +14,11 @@ then XTDA(mf).kernel() (device operator + device Davidson, XTDA.py:746-829).  Ch
 device roots against the eigenvalues (w > 1e-3, XTDA.py:769-772) of the oracle's explicit
 X-TDA matrix (oracle.xtda.full_diag_matrix, XTDA.py:56-400) on the same mean field, and a
 residual |A x - e x| per root through a fresh device A.x.  Writes one JSON record.
+
+--kind xsf: XSF_TDA(mf, SA).kernel() instead (the spin-flip-down, spin-adapted operator of
+BASELINE C4 / C4d; ALDA0 kernel, OO block removed for ROKS, XSF_TDA.py:1501-1554), checked
+against the lowest eigenvalues of the oracle's explicit XSF matrix (XSF_TDA.get_Amat,
+XSF_TDA.py:265-395, oracle.xsf_tda.XSFOracle.get_amat + remove) with the same fglobal.
 """
 import argparse
 import dataclasses
@@ -60,6 +66,8 @@ def main():
     ap.add_argument("--nstates", type=int, default=None,
                     help="roots the Davidson solves for (>= nroots; the Koopmans guess of the lowest gaps "
                          "may miss a symmetry block, XTDA.py:700-734)")
+    ap.add_argument("--kind", default="xtda", choices=("xtda", "xsf"))
+    ap.add_argument("--sa", type=int, default=0, help="XSF spin adaptation (doublets: 0)")
     ap.add_argument("--xc", default="b3lyp")
     ap.add_argument("--tol", type=float, default=1e-12, help="Cholesky tolerance of the exact ERIs")
     ap.add_argument("--conv", type=float, default=1e-10)
@@ -72,7 +80,7 @@ def main():
     import torch
     from xtddft_amd.qc import M, ROKS
     from xtddft_amd.xtda import XTDA
-    rec = dict(molecule=spec["label"], xc=a.xc, chol_tol=a.tol, nroots=nroots, nstates=nstates)
+    rec = dict(molecule=spec["label"], kind=a.kind, xc=a.xc, chol_tol=a.tol, nroots=nroots, nstates=nstates)
     t0 = time.perf_counter()
     mol = M(spec["atom"], basis=spec["basis"], charge=spec["charge"], spin=spec["spin"])
     rec.update(nao=mol.nao, natm=mol.natm, nelectron=mol.nelectron)
@@ -95,19 +103,31 @@ def main():
     mfield = mf.to_meanfield()
     torch.cuda.synchronize()
     rec["meanfield_s"] = round(time.perf_counter() - t0, 3)
-    td = XTDA(None, mfield, nstates=nstates)
-    t0 = time.perf_counter()
-    e = np.asarray(td.kernel())
-    torch.cuda.synchronize()
-    op = td.operator()
-    rec.update(xtda_s=round(time.perf_counter() - t0, 3), xtda_converged=bool(np.all(td.converged)),
-               operator_setup_s=_rounded(dict(op.setup_s)),
-               dim=int(op.dim), k_mode=op.k_mode, naux_cholesky=op.naux()[0],
-               roots_ha=[float(x) for x in e])
-    x = td.v[np.argsort(td.order), :].T          # back to PySCF order
-    ax = op.apply(np.ascontiguousarray(x))
-    rec["max_residual"] = float(np.linalg.norm(ax - e[:, None] * x, axis=1).max())
-    print("xtda", rec["xtda_s"], rec["dim"], e[:5], flush=True)
+    if a.kind == "xsf":
+        from xtddft_amd.xsf_tda import XSF_TDA
+        td = XSF_TDA(mfield, SA=a.sa)
+        t0 = time.perf_counter()
+        td.kernel(nstates=nstates)
+        torch.cuda.synchronize()
+        e = np.asarray(td.e)
+        rec.update(xtda_s=round(time.perf_counter() - t0, 3), xtda_converged=bool(np.all(td.converged)),
+                   fglobal=td.fglobal, sa=a.sa, remove=bool(td.re), davidson_iterations=int(td.icyc),
+                   roots_ha=[float(x) for x in e])
+        print("xsf", rec["xtda_s"], e[:5], flush=True)
+    else:
+        td = XTDA(None, mfield, nstates=nstates)
+        t0 = time.perf_counter()
+        e = np.asarray(td.kernel())
+        torch.cuda.synchronize()
+        op = td.operator()
+        rec.update(xtda_s=round(time.perf_counter() - t0, 3), xtda_converged=bool(np.all(td.converged)),
+                   operator_setup_s=_rounded(dict(op.setup_s)),
+                   dim=int(op.dim), k_mode=op.k_mode, naux_cholesky=op.naux()[0],
+                   roots_ha=[float(x) for x in e])
+        x = td.v[np.argsort(td.order), :].T          # back to PySCF order
+        ax = op.apply(np.ascontiguousarray(x))
+        rec["max_residual"] = float(np.linalg.norm(ax - e[:, None] * x, axis=1).max())
+        print("xtda", rec["xtda_s"], rec["dim"], e[:5], flush=True)
     if not a.no_oracle:
         import threading
         from oracle import xtda as oxtda
@@ -121,11 +141,21 @@ def main():
         threading.Thread(target=heartbeat, daemon=True).start()
         mfo = dataclasses.replace(mfield, cderi=_host(mfield.cderi),
                                   grids=Grid(ao=_host(mfield.grids.ao), weights=_host(mfield.grids.weights)),
-                                  fxc=_host(mfield.fxc))
-        A = oxtda.full_diag_matrix(mfo)
+                                  fxc=_host(mfield.fxc),
+                                  fxc_sf=None if mfield.fxc_sf is None else _host(mfield.fxc_sf))
+        if a.kind == "xsf":
+            from oracle import xsf_tda as oxsf
+            o = oxsf.XSFOracle(mfo, SA=a.sa)
+            A = o.get_amat(foo=1.0, fglobal=oxsf.default_fglobal(mfo))
+            if o.re:
+                A = o.remove(A)
+            rec["dim"] = int(A.shape[0])
+        else:
+            A = oxtda.full_diag_matrix(mfo)
         rec["oracle_symmetry"] = float(np.abs(A - A.T).max() / np.abs(A).max())
         wall = np.linalg.eigvalsh(0.5 * (A + A.T))
-        wall = wall[wall > 1e-3]
+        if a.kind != "xsf":
+            wall = wall[wall > 1e-3]
         w = wall[:nroots]
         rec["oracle_s"] = round(time.perf_counter() - t0, 1)
         rec["oracle_roots_ha"] = [float(v) for v in w]
@@ -135,7 +165,7 @@ def main():
         rec["max_abs_diff_nearest_ha"] = float(np.abs(e[:, None] - wall[None, :]).min(axis=1).max())
         done.set()
         print("oracle", rec["oracle_s"], rec["max_abs_diff_ha"], flush=True)
-    out = a.out or f"gpurun_out/molecule_{a.molecule.replace('+', 'p')}.json"
+    out = a.out or f"gpurun_out/molecule_{a.molecule.replace('+', 'p')}{'_xsf' if a.kind == 'xsf' else ''}.json"
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as f:
         json.dump(rec, f, indent=1)
