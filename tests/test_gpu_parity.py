@@ -321,6 +321,23 @@ def test_sf_multicollinear_many_occupied(dev, nc):
     assert rel(op.apply(z), vind(z)) < RTOL
 
 
+@pytest.mark.parametrize("nranks", [4, 5, 8])
+def test_partitioned_operator_at_driver_rank_counts(hiplib, nranks):
+    """The headline's O = 101 occupied rows over 4, 5 and 8 ranks (replicated factor: aux
+    windows + stored-exchange rows, and the direct aux-window partition): the parts sum to
+    the full operator and the oracle at every rank count the scaling run uses."""
+    from xtddft_amd.operator import DeviceOperator
+    mf = make_mf(nao=130, nc=99, no=2, xctype="GGA", hyb=0.25, ngrid=3000)
+    vind, hdiag = oxtda.gen_tda_operation(mf)
+    z = make_trial_vectors(4, hdiag.size)
+    ref = vind(z)
+    for rep in (True, False):
+        parts = [DeviceOperator(mf, "XTDA", k_mode="stored" if rep else "direct", shard=(r, nranks),
+                                replicate_df=rep) for r in range(nranks)]
+        assert rel(sum(p.apply(z) for p in parts), ref) < RTOL
+        del parts
+
+
 @pytest.mark.parametrize("nranks", [2, 3])
 def test_partitioned_stored_exchange_many_rows(hiplib, nranks):
     """Stored exchange over a replicated factor with >= 2 KX_FOLD chunks of occupied rows
