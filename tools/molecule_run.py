@@ -3,6 +3,7 @@
     python tools/molecule_run.py --molecule naphthalene+ [--nroots 20] [--out FILE]
     python tools/molecule_run.py --molecule ch2
     python tools/molecule_run.py --molecule naphthalene+ --kind xsf [--sa 0]
+    python tools/molecule_run.py --molecule naphthalene+ --kind sfup [--method 1]
 
 * naphthalene+ : C10H8+ doublet, cc-pVDZ (180 AOs: the nao of BASELINE config C2's
   def2-SVP), ROKS B3LYP (the reference's default functional, XTDA.py:1526), X-TDA 20 roots;
@@ -19,6 +20,11 @@ residual |A x - e x| per root through a fresh device A.x.  Writes one JSON recor
 BASELINE C4 / C4d; ALDA0 kernel, OO block removed for ROKS, XSF_TDA.py:1501-1554), checked
 against the lowest eigenvalues of the oracle's explicit XSF matrix (XSF_TDA.get_Amat,
 XSF_TDA.py:265-395, oracle.xsf_tda.XSFOracle.get_amat + remove) with the same fglobal.
+
+--kind sfup: SF_TDA(mf, isf=1, method).kernel() (spin-flip up, BASELINE C3's kind; method 1 =
+the multicollinear kernel of C3mc, 50 samples as the reference's Davidson path), checked
+against the oracle's explicit SF-up matrix (SF_TDA_up.get_Amat, SF_TDA.py:448-560) built on
+the same kernel.
 """
 import argparse
 import dataclasses
@@ -66,7 +72,8 @@ def main():
     ap.add_argument("--nstates", type=int, default=None,
                     help="roots the Davidson solves for (>= nroots; the Koopmans guess of the lowest gaps "
                          "may miss a symmetry block, XTDA.py:700-734)")
-    ap.add_argument("--kind", default="xtda", choices=("xtda", "xsf"))
+    ap.add_argument("--kind", default="xtda", choices=("xtda", "xsf", "sfup"))
+    ap.add_argument("--method", type=int, default=0, help="spin-flip XC kernel: 0 ALDA0, 1 multicollinear")
     ap.add_argument("--sa", type=int, default=0, help="XSF spin adaptation (doublets: 0)")
     ap.add_argument("--xc", default="b3lyp")
     ap.add_argument("--tol", type=float, default=1e-12, help="Cholesky tolerance of the exact ERIs")
@@ -103,7 +110,17 @@ def main():
     mfield = mf.to_meanfield()
     torch.cuda.synchronize()
     rec["meanfield_s"] = round(time.perf_counter() - t0, 3)
-    if a.kind == "xsf":
+    if a.kind == "sfup":
+        from xtddft_amd.sf_tda import DAVIDSON_SAMPLES, SF_TDA
+        td = SF_TDA(mfield, isf=1, method=a.method)
+        t0 = time.perf_counter()
+        td.kernel(nstates=nstates)
+        torch.cuda.synchronize()
+        e = np.asarray(td.e)[:nstates]
+        rec.update(xtda_s=round(time.perf_counter() - t0, 3), xtda_converged=bool(np.all(td.converged)),
+                   method=a.method, roots_ha=[float(x) for x in e])
+        print("sfup", rec["xtda_s"], e[:5], flush=True)
+    elif a.kind == "xsf":
         from xtddft_amd.xsf_tda import XSF_TDA
         td = XSF_TDA(mfield, SA=a.sa)
         t0 = time.perf_counter()
@@ -143,7 +160,13 @@ def main():
                                   grids=Grid(ao=_host(mfield.grids.ao), weights=_host(mfield.grids.weights)),
                                   fxc=_host(mfield.fxc),
                                   fxc_sf=None if mfield.fxc_sf is None else _host(mfield.fxc_sf))
-        if a.kind == "xsf":
+        if a.kind == "sfup":
+            from oracle import sf_tda as osf
+            if a.method == 1:        # the kernel the device solve used (pinned on its own, test_qc.py)
+                mfo.fxc_sf_mc = _host(mfield.extra[("fxc_sf_mc", DAVIDSON_SAMPLES)])
+            A = osf.amat_up(mfo, method=a.method)
+            rec["dim"] = int(A.shape[0])
+        elif a.kind == "xsf":
             from oracle import xsf_tda as oxsf
             o = oxsf.XSFOracle(mfo, SA=a.sa)
             A = o.get_amat(foo=1.0, fglobal=oxsf.default_fglobal(mfo))
@@ -154,7 +177,7 @@ def main():
             A = oxtda.full_diag_matrix(mfo)
         rec["oracle_symmetry"] = float(np.abs(A - A.T).max() / np.abs(A).max())
         wall = np.linalg.eigvalsh(0.5 * (A + A.T))
-        if a.kind != "xsf":
+        if a.kind == "xtda":
             wall = wall[wall > 1e-3]
         w = wall[:nroots]
         rec["oracle_s"] = round(time.perf_counter() - t0, 1)
@@ -165,7 +188,8 @@ def main():
         rec["max_abs_diff_nearest_ha"] = float(np.abs(e[:, None] - wall[None, :]).min(axis=1).max())
         done.set()
         print("oracle", rec["oracle_s"], rec["max_abs_diff_ha"], flush=True)
-    out = a.out or f"gpurun_out/molecule_{a.molecule.replace('+', 'p')}{'_xsf' if a.kind == 'xsf' else ''}.json"
+    suffix = "" if a.kind == "xtda" else f"_{a.kind}" + (f"_mc" if a.method == 1 else "")
+    out = a.out or f"gpurun_out/molecule_{a.molecule.replace('+', 'p')}{suffix}.json"
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as f:
         json.dump(rec, f, indent=1)
