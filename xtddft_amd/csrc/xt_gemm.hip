@@ -849,10 +849,11 @@ void plan_gemm(const GemmDesc& d, GemmParams* pp, int* cfg_out) {
     const double e128 = (double)d.N / (128.0 * ((d.N + 127) / 128)), e64 = (double)d.N / (64.0 * ((d.N + 63) / 64));
     if (e128 < 0.75 && e64 - e128 > 0.12) cfg = 4;
   }
-  if (d.tag == 2 || d.tag == 3) {   // tuning hooks (A/B runs): XT_GEMM_U_CFG / XT_GEMM_L_CFG = 2, 3, 4,
-                                    // 5, 8 or 9 for XC forward U / back L
-    const char* e = getenv(d.tag == 2 ? "XT_GEMM_U_CFG" : "XT_GEMM_L_CFG");
-    const int f = e ? atoi(e) : -1;
+  if (d.tag == 2 || d.tag == 3) {   // tuning hooks (A/B runs, read once per process):
+                                    // XT_GEMM_U_CFG / XT_GEMM_L_CFG = 2, 3, 4, 5, 8 or 9
+    static const int forced[2] = {[] { const char* e = getenv("XT_GEMM_U_CFG"); return e ? atoi(e) : -1; }(),
+                                  [] { const char* e = getenv("XT_GEMM_L_CFG"); return e ? atoi(e) : -1; }()};
+    const int f = forced[d.tag - 2];
     if (f == 2 || f == 3 || f == 4 || f == 5 || f == 8 || f == 9) cfg = f;
   }
   const Cfg& c = kCfg[cfg];
