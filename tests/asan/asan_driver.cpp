@@ -48,6 +48,7 @@ int main() {
   expect_err(xt_set_grid(nullptr, buf, buf, buf, XT_PTR_HOST), "set_grid null");
   expect_err(xt_apply(nullptr, 1, buf, buf, XT_PTR_HOST), "apply null");
   expect_err(xt_set_exchange_mode(nullptr, XT_K_AUTO, 0.0), "exchange_mode null");
+  expect_err(xt_exchange_plan(nullptr, nullptr, nullptr), "exchange_plan null");
   expect_err(xt_set_profile(nullptr, 1), "profile null");
   expect_err(xt_profile_stats(nullptr, 1, buf), "profile_stats null");
   expect_err(xt_profile_bytes(nullptr, 9, buf), "profile_bytes bad tag");
