@@ -2,6 +2,7 @@
 new vectors): ms per call and per class (live HIP-event timing) for nvec in --nvecs.
 
     python tools/nvec_sweep.py [--nvecs 1,2,3,4,6,8,12,16,20] [--reps 3] [--out FILE]
+    python tools/nvec_sweep.py --nao 256 --nclosed 24 --nvecs 1,8,20,40,80   (SURVEY 8(d) sweeps)
 """
 import argparse
 import json
@@ -19,10 +20,17 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--config", default="H")
     ap.add_argument("--out", default="gpurun_out/nvec_sweep.json")
+    ap.add_argument("--nao", type=int, default=None)
+    ap.add_argument("--nclosed", type=int, default=None)
+    ap.add_argument("--nopen", type=int, default=None)
     a = ap.parse_args()
     import torch
     import bench
-    args = bench.parse(["--config", a.config])
+    argv = ["--config", a.config]
+    for k in ("nao", "nclosed", "nopen"):
+        if getattr(a, k) is not None:
+            argv += [f"--{k}", str(getattr(a, k))]
+    args = bench.parse(argv)
     w = bench.device_workload(args, 0, 1, 0)
     op = w.op
     rows = []
@@ -42,7 +50,9 @@ def main():
         torch.cuda.synchronize()
         ms = 1e3 * (time.perf_counter() - t0) / a.reps
         op.set_profile(0)
-        r = dict(nvec=nv, ms=round(ms, 2), ms_per_vec=round(ms / nv, 2), classes={k: round(v, 2) for k, v in cls.items()})
+        r = dict(nao=args.nao, nc=args.nc, no=args.no, dim=op.dim, ngrid=args.ngrid, naux=args.naux, nvec=nv,
+                 ms=round(ms, 3), ms_per_vec=round(ms / nv, 3), matvecs_per_s=round(1e3 * nv / ms, 2),
+                 k_mode=getattr(op, "k_mode", None), classes={k: round(v, 3) for k, v in cls.items()})
         rows.append(r)
         print(json.dumps(r), flush=True)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
