@@ -66,10 +66,11 @@ def test_xc_kernel_variants(hiplib, env, knobs, nc, no, nao):
     assert rel(op.apply(z), vind(z)) < RTOL
 
 
-@pytest.mark.parametrize("nz", [13, 41])
+@pytest.mark.parametrize("nz", [13, 30, 41])
 @pytest.mark.parametrize("sa", [2, 3])
 def test_xsf_stored_exchange_blocks(hiplib, nz, sa):
-    """4 nz = 52 rows (160-row tile) and 41 vectors (one 40-vector batch + 1)."""
+    """4 nz = 52 rows (96-row image), 120 rows (128-row image) and 41 vectors (one
+    40-vector batch, 160 rows, + 1)."""
     from xtddft_amd.operator import DeviceOperator
     mf = make_mf(nao=30, nc=6, no=3, xctype="GGA", hyb=0.5)
     o = oxsf.XSFOracle(mf, SA=sa)
@@ -81,10 +82,11 @@ def test_xsf_stored_exchange_blocks(hiplib, nz, sa):
     assert rel(op.apply(z), vind(z)) < RTOL
 
 
-@pytest.mark.parametrize("nz", [17, 20, 23])
+@pytest.mark.parametrize("nz", [17, 20, 23, 25, 48, 49, 64, 65])
 def test_stored_exchange_row_shapes(hiplib, nz):
     """2 nz = 34 / 40 rows: the 32 MFMA rows + VALU remainder shape of the streaming
-    exchange kernel; 46 rows: the 48-row MFMA shape."""
+    exchange kernel; 46 rows: the 48-row MFMA shape; 50 / 96 rows the 96-row image, 98 / 128
+    the 128-row image, 130 the 160-row image."""
     from xtddft_amd.operator import DeviceOperator
     mf = make_mf(nao=40, nc=8, no=2, ngrid=2000, xctype="GGA", hyb=0.25)
     vind, hdiag = oxtda.gen_tda_operation(mf)

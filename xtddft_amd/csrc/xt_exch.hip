@@ -33,9 +33,10 @@ namespace xt {
 typedef double d4x __attribute__((ext_vector_type(4)));
 typedef double d2x __attribute__((ext_vector_type(2)));
 
-// Two shapes: <3, 4, 64> (M <= 48: the X-TDA / SF exchange, 2 nz or nz rows; two
-// blocks per CU) and <10, 2, 32> (M <= 160: the XSF exchange with its four
-// spin-adaptation source blocks, 4 nz rows; one block per CU, 160 accumulator VGPRs).
+// Two families: <1..3, 4, 64> (M <= 48: the X-TDA / SF exchange, 2 nz or nz rows; two
+// blocks per CU) and <6 | 8 | 10, 2, 32> (M <= 96 / 128 / 160: larger batches and the XSF
+// exchange with its four spin-adaptation source blocks, 4 nz rows; one block per CU, up to
+// 160 accumulator VGPRs).
 constexpr int SK_WAVES = 8;
 constexpr int SK_MAXM = 160;
 
@@ -250,10 +251,16 @@ struct SkShape { int mp, bn, bk, slots; };
 // a Davidson step with few new vectors streams Kx without the padded rows' MFMAs
 // (M = 2 nz <= 16 through 48 rows made the stream matrix-pipe bound).  M = 33..40
 // takes 32 MFMA rows + the VALU remainder rows (48-row image).
+// Past 48 rows the one-block-per-CU shape of 2 MFMA column sub-tiles per wave, in the
+// smallest of 96 / 128 / 160 rows that covers M (X-TDA Davidson steps of 25-80 vectors,
+// XSF steps of 13-40: M = 2 nz or 4 nz; headline operator, same box: 30 vectors 37.8 ->
+// 22.6 ms, 40 vectors 37.8 -> 23.9 ms per A.x; C4's 20-root solve 10.17-10.20 -> 10.01 s).
 SkShape sk_shape(int M) {
   if (M <= 16) return {16, 16 * 4 * SK_WAVES, 64, 2};
   if (M <= 32) return {32, 16 * 4 * SK_WAVES, 64, 2};
   if (M <= 48) return {48, 16 * 4 * SK_WAVES, 64, 2};
+  if (M <= 96) return {96, 16 * 2 * SK_WAVES, 32, 1};
+  if (M <= 128) return {128, 16 * 2 * SK_WAVES, 32, 1};
   return {160, 16 * 2 * SK_WAVES, 32, 1};
 }
 }  // namespace
@@ -319,6 +326,12 @@ int skinny_gemm(int M, int N, int K, double alpha, const double* A, long lda, co
   else if (sh.mp == 48)
     hipLaunchKernelGGL((k_skinny<3, 4, 64, 4>), dim3(strips, used), dim3(512), 0, st, N, K, kchunk, AT, B, ldb, part,
                        (long)N);
+  else if (sh.mp == 96)
+    hipLaunchKernelGGL((k_skinny<6, 2, 32, 4>), dim3(strips, used), dim3(512), 0, st, N, K, kchunk, AT, B, ldb,
+                       part, (long)N);
+  else if (sh.mp == 128)
+    hipLaunchKernelGGL((k_skinny<8, 2, 32, 4>), dim3(strips, used), dim3(512), 0, st, N, K, kchunk, AT, B, ldb,
+                       part, (long)N);
   else
     hipLaunchKernelGGL((k_skinny<10, 2, 32, 4>), dim3(strips, used), dim3(512), 0, st, N, K, kchunk, AT, B, ldb,
                        part, (long)N);
