@@ -338,17 +338,18 @@ def test_partitioned_operator_at_driver_rank_counts(hiplib, nranks):
         del parts
 
 
+@pytest.mark.parametrize("nz", [4, 30])
 @pytest.mark.parametrize("nranks", [2, 3])
-def test_partitioned_stored_exchange_many_rows(hiplib, nranks):
+def test_partitioned_stored_exchange_many_rows(hiplib, nranks, nz):
     """Stored exchange over a replicated factor with >= 2 KX_FOLD chunks of occupied rows
     per rank (O = 48 over 2 and 3 ranks): the symmetric build's mirror runs for row blocks
     that start past 0 (i0 > 0), and each partitioned context drops the factor rows outside
     its aux window after the build (xt_prepare).  The summed parts equal the full operator
-    and the oracle."""
+    and the oracle; 2 nz = 8 and 60 stream rows (the 16- and 96-row images)."""
     from xtddft_amd.operator import DeviceOperator
     mf = make_mf(nao=80, nc=46, no=2, xctype="GGA", hyb=0.25, ngrid=2000)
     vind, hdiag = oxtda.gen_tda_operation(mf)
-    z = make_trial_vectors(4, hdiag.size)
+    z = make_trial_vectors(nz, hdiag.size)
     full = DeviceOperator(mf, "XTDA", k_mode="stored")
     parts = [DeviceOperator(mf, "XTDA", k_mode="stored", shard=(r, nranks), replicate_df=True)
              for r in range(nranks)]
