@@ -138,7 +138,13 @@ class Mole:
         self._nao = int(self.ao_loc[-1])
         self.symmetry = self._check_symmetry(symmetry)
         self._norm = None
-        self._norm = 1.0 / np.sqrt(np.diag(self._intor_raw("ovlp")))
+        self._int1e = {}
+        # AO norms need only the diagonal shell blocks <a|a>
+        diag = np.empty(self._nao)
+        for s, p0 in zip(self.shells, self.ao_loc[:-1]):
+            T = _sph_transform(s.l)
+            diag[p0:p0 + s.nsph] = np.diag(T @ ShellPair(s, s, hermite=False).overlap() @ T.T)
+        self._norm = 1.0 / np.sqrt(diag)
 
     # -------------------------------------------------------------- basics
     def nao_nr(self) -> int:
@@ -206,8 +212,32 @@ class Mole:
         return out
 
     # ----------------------------------------------------------- integrals
+    def _ovlp_kin(self):
+        """int1e_ovlp and int1e_kin in one pass over the shell pairs (the pair's
+        Hermite tables, extended for the kinetic operator, serve both); cached."""
+        if "kin" not in self._int1e:
+            n = self._nao
+            S, T = np.zeros((n, n)), np.zeros((n, n))
+            sh = self.shells
+            for i, si in enumerate(sh):
+                Ti = _sph_transform(si.l)
+                a0, a1 = self.ao_loc[i], self.ao_loc[i + 1]
+                for j in range(i + 1):
+                    Tj = _sph_transform(sh[j].l)
+                    b0, b1 = self.ao_loc[j], self.ao_loc[j + 1]
+                    pair = ShellPair(si, sh[j], kin=True, hermite=False)
+                    for out, blk in ((S, pair.overlap()), (T, pair.kinetic())):
+                        blk = Ti @ blk @ Tj.T
+                        out[a0:a1, b0:b1] = blk
+                        out[b0:b1, a0:a1] = blk.T
+            nrm = self._norm[:, None] * self._norm[None, :]
+            self._int1e["ovlp"], self._int1e["kin"] = S * nrm, T * nrm
+        return self._int1e["ovlp"].copy(), self._int1e["kin"].copy()
+
     def _intor_raw(self, kind, origin=(0.0, 0.0, 0.0)):
         n = self._nao
+        if kind in ("ovlp", "kin") and self._norm is not None:
+            return self._ovlp_kin()[0 if kind == "ovlp" else 1]
         if kind in ("r", "ipovlp", "irxp"):
             out = np.zeros((3, n, n))
         else:

@@ -165,7 +165,7 @@ class ShellPair:
     p[q], P[q, 3]          combined exponents / centres.
     """
 
-    def __init__(self, sa, sb, kin: bool = False):
+    def __init__(self, sa, sb, kin: bool = False, hermite: bool = True):
         self.sa, self.sb = sa, sb
         la, lb = sa.l, sb.l
         a = sa.exps[:, None]
@@ -179,6 +179,9 @@ class ShellPair:
         cc = (sa.coefs[:, None] * sb.coefs[None, :]).ravel()
         self.cc = cc
         L = la + lb
+        self.L = L
+        if not hermite:          # one-electron overlap-type integrals need only the 1D tables
+            return
         tuv, _ = hermite_index(L)
         ca, cb = cart_comps(la), cart_comps(lb)
         Eab = np.zeros((len(ca), len(cb), len(tuv), self.p.size))
@@ -190,7 +193,6 @@ class ShellPair:
                         continue
                     Eab[i, j, k] = Ex[ax, bx, t] * Ey[ay, by, u] * Ez[az, bz, v] * cc
         self.Eab = Eab
-        self.L = L
 
     # 1D overlap table S[i, j] over primitive pairs, with the sqrt(pi/p) factor
     def _s1d(self, d):
