@@ -50,9 +50,12 @@ sys.path.insert(0, ROOT)
 
 FP64_PEAK_TFLOPS = 78.6     # MI355X dense FP64 matrix peak (AMD spec); 74.2 measured (tools/mfma_probe.hip)
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8.0 TB/s spec
-# the newest committed rocprofv3 FETCH / WRITE summary (tools/parse_prof.py)
-# committed rocprofv3 PMC summaries, newest round first
-PMC_SUMMARIES = [os.path.join(ROOT, "profiles", f"r0{k}_pmc_summary.json") for k in (5, 4)]
+# this round's committed rocprofv3 FETCH / WRITE summary (tools/parse_prof.py): the only one
+# roofline.traffic is read from (an older round's bytes would describe older kernels)
+ROUND = 6
+PMC_SUMMARY = os.path.join(ROOT, "profiles", f"r{ROUND:02d}_pmc_summary.json")
+
+CPU_CONVERGE_AUTO_S = 60.0   # bench's default run times the CPU Davidson only when it is this short
 
 KIND_NAME = {"XTDA": "X-TDA", "SF_UP": "SF-TDA (spin-flip up)", "SF_DOWN": "SF-TDA (spin-flip down)",
              "XSF": "XSF-TDA"}
@@ -105,6 +108,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-converge", action="store_true")
     ap.add_argument("--converge", action="store_true", help="force the Davidson run (default on; see --no-converge)")
+    ap.add_argument("--cpu-converge", default="auto", choices=["auto", "on", "off"],
+                    help="time the oracle Davidson to nroots on the host (auto: when the CPU A.x "
+                         "rate puts it under CPU_CONVERGE_AUTO_S)")
     ap.add_argument("--k-mode", default="auto", choices=["auto", "direct", "stored"],
                     help="exchange evaluation (xt_set_exchange_mode)")
     args = ap.parse_args(argv)
@@ -259,7 +265,7 @@ def _host_info():
     return info
 
 
-def _oracle_vind(args, mf):
+def _oracle_vind(args, mf, with_hdiag=False):
     from oracle import sf_tda as osf
     from oracle import xsf_tda as oxsf
     from oracle import xtda as oxtda
@@ -271,8 +277,8 @@ def _oracle_vind(args, mf):
     o.re = bool(args.remove)
     if o.re and o.no > 1:
         o.vects = oxsf.get_vect(o.no)
-    # the preconditioner's J diagonals are solver setup, not A.x: not built here
-    return o.gen_tda_operation_sf(fglobal=0.7 * args.hyb + 0.3, with_hdiag=False)
+    # the preconditioner's J diagonals are solver setup, not A.x: built only for a solve
+    return o.gen_tda_operation_sf(fglobal=0.7 * args.hyb + 0.3, with_hdiag=with_hdiag)
 
 
 def log(msg):
@@ -396,10 +402,10 @@ def cpu_baseline(args, w, z0, s0):
 # ---------------------------------------------------------------------------
 # Davidson to nroots on the same operator (reference criteria per kind)
 # ---------------------------------------------------------------------------
-def converge(args, w, allreduce):
-    import torch
-    from xtddft_amd.davidson import DiagPrecond, davidson1
-    mf, op, dev = w.mf, w.op, w.device
+def _solver_setup(args, w, dev):
+    """(x0, preconditioner, davidson1 keywords, criteria) of the device solve, per kind."""
+    mf, op = w.mf, w.op
+    from xtddft_amd.davidson import DiagPrecond
     if args.kind == "XTDA":
         from xtddft_amd.xtda import XTDA
         x = XTDA.__new__(XTDA)
@@ -411,30 +417,35 @@ def converge(args, w, allreduce):
             idx = np.where(wv > 0.001)[0]
             return wv[idx], v[:, idx], idx
         kw = dict(tol_residual=1e-5, lindep=1e-12, pick=pickeig, max_cycle=100)
-        pre = DiagPrecond(hdiag, 0.0, dev.index)
-        crit = "|de|<1e-12, |r|<1e-5, pick w>1e-3 (XTDA.py:769-777)"
-    elif args.kind in ("SF_UP", "SF_DOWN"):
+        return x0, DiagPrecond(hdiag, 0.0, dev.index), kw, "|de|<1e-12, |r|<1e-5, pick w>1e-3 (XTDA.py:769-777)"
+    if args.kind in ("SF_UP", "SF_DOWN"):
         from xtddft_amd.sf_tda import init_guess, sf_hdiag
         isf = 1 if args.kind == "SF_UP" else -1
-        hdiag = sf_hdiag(mf, isf)
         x0 = init_guess(mf, args.nroots, isf)
-        kw = dict(tol=1e-7, lindep=1e-14, max_cycle=3000)
-        pre = DiagPrecond(hdiag, 1e-3, dev.index)
-        crit = "tol 1e-7, lindep 1e-14 (SF_TDA.py:392-395)"
-    else:
-        from xtddft_amd.xsf_tda import XSF_TDA, get_vect
-        x = XSF_TDA(mf, SA=args.sa, device=dev.index)
-        x.re = bool(args.remove)
-        x.vects = get_vect(args.no)
-        x.nstates = args.nroots
-        fg = 0.7 * args.hyb + 0.3
-        hdiag = x._build_preconditioner_hdiag(fg, op)
-        if x.re:
-            hdiag = x._compress_removed_hdiag(hdiag)
-        x0 = x.init_guess(args.nroots, hdiag)
-        kw = dict(tol=1e-8, lindep=1e-9, max_cycle=1000)
-        pre = DiagPrecond(hdiag, 1e-3, dev.index)
-        crit = "tol 1e-8, lindep 1e-9 (XSF_TDA.py:1467-1470)"
+        return (x0, DiagPrecond(sf_hdiag(mf, isf), 1e-3, dev.index), dict(tol=1e-7, lindep=1e-14, max_cycle=3000),
+                "tol 1e-7, lindep 1e-14 (SF_TDA.py:392-395)")
+    from xtddft_amd.xsf_tda import XSF_TDA, get_vect
+    x = XSF_TDA(mf, SA=args.sa, device=dev.index)
+    x.re = bool(args.remove)
+    x.vects = get_vect(args.no)
+    x.nstates = args.nroots
+    hdiag = x._build_preconditioner_hdiag(0.7 * args.hyb + 0.3, op)
+    if x.re:
+        hdiag = x._compress_removed_hdiag(hdiag)
+    x0 = x.init_guess(args.nroots, hdiag)
+    return (x0, DiagPrecond(hdiag, 1e-3, dev.index), dict(tol=1e-8, lindep=1e-9, max_cycle=1000),
+            "tol 1e-8, lindep 1e-9 (XSF_TDA.py:1467-1470)")
+
+
+def converge(args, w, allreduce, world=1):
+    """Wall time of the device Davidson to nroots under the reference's criteria (operator
+    construction included).  An untimed 2-iteration solve first loads the solver's kernels
+    (first-launch costs are not per-solve work); the replicated solver of a sharded
+    operator runs with the lockstep guard."""
+    import torch
+    from xtddft_amd.davidson import davidson1
+    op, dev = w.op, w.device
+    x0, pre, kw, crit = _solver_setup(args, w, dev)
     stats = dict(calls=0, vectors=0, s=0.0, allreduce_s=0.0, nvec=[])
 
     def aop(xt):
@@ -450,46 +461,88 @@ def converge(args, w, allreduce):
         stats["s"] += t1 - t
         stats["allreduce_s"] += time.perf_counter() - t1
         return s
+    warm = dict(kw, max_cycle=2)
+    davidson1(lambda xt: allreduce(op.apply(xt)), x0, pre, nroots=args.nroots, device=dev.index,
+              return_device=True, lockstep=world > 1, **warm)
     torch.cuda.synchronize()
     log(f"converging {args.nroots} roots")
     tc = time.perf_counter()
     conv, e, _, icyc = davidson1(aop, x0, pre, nroots=args.nroots, device=dev.index,
-                                 return_device=True, **kw)
+                                 return_device=True, lockstep=world > 1, **kw)
     torch.cuda.synchronize()
     wall = time.perf_counter() - tc
     hist = {}
     for k in stats["nvec"]:
         hist[k] = hist.get(k, 0) + 1
+    host = wall - stats["s"] - stats["allreduce_s"]
     return dict(nroots=args.nroots, wall_s=round(wall + w.t_op, 2), davidson_s=round(wall, 2),
                 operator_setup_s=round(w.t_op, 2), iterations=int(icyc) + 1,
                 converged=bool(np.all(conv)), ax_calls=stats["calls"], ax_vectors=stats["vectors"],
                 ax_s=round(stats["s"], 3), allreduce_s=round(stats["allreduce_s"], 3),
-                host_davidson_s=round(wall - stats["s"] - stats["allreduce_s"], 3),
+                host_davidson_s=round(host, 4), host_ms_per_iteration=round(1e3 * host / (int(icyc) + 1), 3),
                 nvec_histogram={str(k): v for k, v in sorted(hist.items())},
-                e_min_ha=float(e[0]), criteria=crit)
+                e_min_ha=float(e[0]), e_ha=[float(v) for v in e], criteria=crit,
+                warmup="an untimed 2-iteration solve first (solver kernels loaded)")
+
+
+def cpu_converge(args, w, gpu):
+    """The CPU side of wall-to-converge (SURVEY.md 8(d) "both sides"): the oracle Davidson
+    (oracle/davidson.py, the reference's davidson1 restated, Davidson.py:21-298) driving the
+    oracle vind (the reference's AO route) on the SAME data, x0, preconditioner and criteria
+    as the device solve, on every CPU of this process's share.  Operator construction (the
+    oracle's Fock / hdiag set-up) is included, as on the device side."""
+    from threadpoolctl import threadpool_info, threadpool_limits
+    from oracle import davidson as odav
+    ncpu = cpu_share()
+    with threadpool_limits(limits=ncpu):
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()
+                       if i.get("user_api") == "blas"] or [1])
+        mfo, _ = oracle_meanfield(args, w)
+        log(f"cpu converge: {args.nroots} roots, oracle Davidson on {threads} BLAS threads")
+        t0 = time.perf_counter()
+        calls = dict(n=0, v=0)
+        vind, hd = _oracle_vind(args, mfo, with_hdiag=args.kind == "XSF")
+
+        def aop(xt):
+            calls["n"] += 1
+            calls["v"] += len(xt)
+            log(f"cpu converge: A.x call {calls['n']} ({len(xt)} vectors, {time.perf_counter() - t0:.0f} s)")
+            return vind(xt)
+        x0, pre, kw, crit = _solver_setup(args, w, w.device)
+        if args.kind == "XTDA":
+            from oracle import xtda as oxtda
+            precond, kw = oxtda.get_precond(mfo, hd), dict(kw, pick=oxtda.pickeig)
+        else:
+            precond = odav.make_diag_precond(hd, 1e-3)
+        conv, e, _, icyc = odav.davidson1(aop, x0, precond, nroots=args.nroots, **kw)
+        wall = time.perf_counter() - t0
+    e = np.asarray(e)
+    return dict(converge_wall_s=round(wall, 2), iterations=int(icyc) + 1, converged=bool(np.all(conv)),
+                ax_calls=calls["n"], ax_vectors=calls["v"], cores=int(threads), kind="port",
+                e_min_ha=float(e[0]), max_abs_de_vs_gpu_ha=float(np.abs(e - np.asarray(gpu["e_ha"])).max()),
+                gpu_over_cpu_speedup=round(wall / gpu["wall_s"], 1), criteria=crit,
+                sample=("oracle Davidson + oracle vind (NumPy AO route) on the timed operator's own data, "
+                        "same x0 / preconditioner / criteria as the device solve, full size"))
 
 
 # ---------------------------------------------------------------------------
 def load_traffic(config, tag_name):
-    """HBM bytes per launch of the tagged kernel from the newest committed rocprofv3 PMC
-    summary (profiles/r0*_pmc_summary.json) that holds this config and class, None if none."""
-    for path in PMC_SUMMARIES:
-        try:
-            with open(path) as f:
-                d = json.load(f)
-        except (OSError, ValueError):
-            continue
-        v = d.get(config, {}).get(tag_name, {}).get("hbm_bytes_per_launch")
-        if v is not None:
-            return v
-    return None
+    """(HBM bytes per launch of the tagged kernel, source file) from this round's committed
+    rocprofv3 PMC summary; (None, None) when it does not hold this config and class."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    v = d.get(config, {}).get(tag_name, {}).get("hbm_bytes_per_launch")
+    return (v, os.path.relpath(PMC_SUMMARY, ROOT)) if v is not None else (None, None)
 
 
 def roofline_of(args, stats_acc, steps, world=1):
     dom_name, dom = max(stats_acc.items(), key=lambda kv: kv[1]["ms"])
     avg_ms = dom["ms"] / max(1, dom["launches"])
     # the committed PMC summaries are single-GPU runs of the presets
-    traffic = None if (args.custom or world > 1) else load_traffic(args.config, dom_name)
+    traffic, source = (None, None) if (args.custom or world > 1) else load_traffic(args.config, dom_name)
     if dom_name == "mo_exchange_stored":
         # HBM-bound: streams the stored exchange matrix once per launch (+ Ze in, sigma in/out)
         occ = args.nc if args.kind == "SF_UP" else args.nc + args.no
@@ -499,7 +552,7 @@ def roofline_of(args, stats_acc, steps, world=1):
         bytes_launch = 8.0 * (ov * ov + 3.0 * nzg * ov)
         gbs = bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         return dict(bound="hbm", achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=round(gbs / HBM_PEAK_GBS, 4), traffic=traffic, kernel=dom_name,
+                    frac=round(gbs / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=source, kernel=dom_name,
                     avg_launch_ms=round(avg_ms, 4), bytes_per_launch=bytes_launch,
                     launches_per_step=dom["launches"] / steps)
     flops_fused = dom["flops"] / max(1, dom["launches"])
@@ -510,7 +563,7 @@ def roofline_of(args, stats_acc, steps, world=1):
     achieved = flops_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     fused = flops_fused / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     return dict(bound="mfma", achieved=round(achieved, 3), peak=FP64_PEAK_TFLOPS, unit="TFLOP/s",
-                frac=round(achieved / FP64_PEAK_TFLOPS, 4), traffic=traffic,
+                frac=round(achieved / FP64_PEAK_TFLOPS, 4), traffic=traffic, traffic_source=source,
                 kernel=dom_name, avg_launch_ms=round(avg_ms, 4),
                 flops_per_launch=flops_launch, launches_per_step=dom["launches"] / steps,
                 accounting="strict: 2 G nvec sum_s o_s v_s (SURVEY.md 8(d))",
@@ -666,7 +719,7 @@ def rank_main(args):
         if not v["launches"]:
             continue
         comp = v["bytes"] / v["launches"]
-        hbm = None if (args.custom or world > 1) else load_traffic(args.config, k)
+        hbm = None if (args.custom or world > 1) else load_traffic(args.config, k)[0]
         others[k] = dict(ms_per_step=round(v["ms"] / args.steps, 3),
                          tflops=round(v["flops"] * strict_factor(args, k) / max(v["ms"], 1e-9) / 1e9, 3),
                          tflops_fused_accounting=round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 3),
@@ -715,8 +768,19 @@ def rank_main(args):
         except Exception as e:   # report, never hide
             result["cpu_baseline"] = dict(value=None, error=repr(e))
     if use_gpu and (not args.no_converge or args.converge):
-        result["converge"] = converge(args, w, allreduce_sigma)
+        result["converge"] = converge(args, w, allreduce_sigma, world)
         mine["converge"] = {k: result["converge"][k] for k in ("ax_s", "allreduce_s", "host_davidson_s")}
+        cpu = result.get("cpu_baseline") or {}
+        est = result["converge"]["ax_vectors"] / cpu["value"] if cpu.get("value") else None
+        if rank == 0 and world == 1 and (args.cpu_converge == "on" or (
+                args.cpu_converge == "auto" and est is not None and est < CPU_CONVERGE_AUTO_S)):
+            try:
+                cpu["converge"] = cpu_converge(args, w, result["converge"])
+            except Exception as e:   # report, never hide
+                cpu["converge"] = dict(error=repr(e))
+            result["cpu_baseline"] = cpu
+        elif rank == 0 and world == 1 and est is not None:
+            cpu["converge"] = dict(skipped=f"estimated {est:.0f} s of CPU A.x (--cpu-converge on runs it)")
     if pg:
         ranks = [None] * world
         dist.all_gather_object(ranks, mine)

@@ -142,7 +142,8 @@ int xt_set_exchange_mode(xt_ctx* ctx, int mode, double max_gib);
    the factor set again. */
 int xt_prepare(xt_ctx* ctx, int* k_mode, double* k_gib);
 /* What XT_K_AUTO resolves to on this context (*stored = 1 / 0) and the stored
-   matrix's footprint (GiB), without building anything.  The resolution depends
+   matrix's footprint (GiB; 0 for an operator without exchange), without building
+   anything.  The resolution depends
    on this GPU's free HBM, so the ranks of a partitioned operator must agree
    before they build: a rank that streams its stored ROWS and a rank that
    contracts its aux WINDOW directly do not sum to the operator.  The host side

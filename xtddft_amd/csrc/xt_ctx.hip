@@ -982,7 +982,7 @@ extern "C" int xt_exchange_plan(xt_ctx* c, int* stored, double* k_gib) {
   (void)hipSetDevice(c->d.device);
   RET(resolve_kmode(c));
   if (stored) *stored = c->k_resolved == 1 ? 1 : 0;
-  if (k_gib) *k_gib = kx_doubles(c) * 8.0 / (double)((size_t)1 << 30);
+  if (k_gib) *k_gib = has_exchange(c) ? kx_doubles(c) * 8.0 / (double)((size_t)1 << 30) : 0.0;
   return 0;
 }
 

@@ -21,11 +21,19 @@ returning the 4-tuple ``(conv, e, x, icyc)`` its callers unpack
 * only the small ``heff`` (<= (max_space+nroots)^2) crosses to the host for
   ``scipy.linalg.eigh`` (Davidson.py:199), as in the reference.
 
-``aop`` receives and returns device tensors of shape (n, dim).  Under a
-torch.distributed group (the replicated solver of a sharded operator) every
-iteration's decisions are gathered and compared across ranks
-(``parallel.lockstep_check``): a divergence raises on all ranks instead of
-leaving some waiting in the next all-reduce.  ``precond``
+``aop`` receives and returns device tensors of shape (n, dim).  For the replicated
+solver of a sharded operator (``lockstep=True``, which the drivers pass when their
+shard spans more than one rank) every iteration's decisions are gathered and compared
+across the ranks of ``group`` (``parallel.lockstep_check``): a divergence raises on all
+ranks instead of leaving some waiting in the next all-reduce.  An unsharded solve
+never communicates, whatever process group exists.
+
+Host cost per iteration (the part that does not shrink with more GPUs): four device ->
+host round trips (heff rows, residual norms, the Gram matrix of the new block -- its
+diagonal is the drop test of ``_normalize_xt_`` and it seeds the next ``_qr`` -- and the
+Cholesky-QR pass), and the small host LAPACK (heff ``eigh``, the coefficient-space
+Gram-Schmidt) on one BLAS thread: a multithreaded BLAS is slower on matrices of this
+size (measured: eigh of 70 x 70 at 0.6 ms on one thread, up to 8 ms on eight).  ``precond``
 may be a diagonal (array or device tensor: PySCF ``make_diag_precond`` with
 level shift 1e-3), a ``DiagPrecond`` (device kernel), or any host callable
 ``precond(dx, e, x0)`` (evaluated on host copies).
@@ -50,6 +58,18 @@ class LinearDependenceError(RuntimeError):
 def _torch():
     import torch
     return torch
+
+
+_BLAS_CTL = None
+
+
+def _one_blas_thread():
+    """Context limiting the host BLAS to one thread (cached controller: ~15 us per use)."""
+    global _BLAS_CTL
+    if _BLAS_CTL is None:
+        from threadpoolctl import ThreadpoolController
+        _BLAS_CTL = ThreadpoolController()
+    return _BLAS_CTL.limit(limits=1, user_api="blas")
 
 
 class DiagPrecond:
@@ -167,7 +187,7 @@ def _qr_vectorwise(dev, x, lindep):
     return out[:kept]
 
 
-def _qr(dev, x, lindep):
+def _qr(dev, x, lindep, gram=None):
     """Orthonormalise the rows of x in order, dropping dependent ones (PySCF
     _qr, Davidson.py:152,172).  Block form with two host round trips instead
     of one per vector: the Gram matrix x x^T (device GEMM) drives Gram-Schmidt
@@ -175,15 +195,19 @@ def _qr(dev, x, lindep):
     the device, then one Cholesky-QR pass Q = L^-1 Q1 (L L^T = Q1 Q1^T)
     restores orthogonality to round-off (CholQR2 pattern).  Nearly dependent
     rows (a kept residual norm**2 below GRAM_SAFE_NORM2) or a failed Cholesky take
-    the vector-by-vector path (``_qr_vectorwise``)."""
+    the vector-by-vector path (``_qr_vectorwise``).  ``gram``: x x^T when the caller
+    already holds it on the host (saves one round trip)."""
     torch = dev.torch
     n, dim = x.shape
     if n == 0:
         return x
     x = x.contiguous()
-    g = torch.empty((n, n), dtype=torch.float64, device=dev.device)
-    dev.gemm(0, 1, n, n, dim, 1.0, x, dim, x, dim, 0.0, g, n)
-    c, nmin = _gram_gs(g.cpu().numpy(), lindep)
+    if gram is None:
+        g = torch.empty((n, n), dtype=torch.float64, device=dev.device)
+        dev.gemm(0, 1, n, n, dim, 1.0, x, dim, x, dim, 0.0, g, n)
+        gram = g.cpu().numpy()
+    with _one_blas_thread():
+        c, nmin = _gram_gs(gram, lindep)
     k = c.shape[0]
     if k == 0:
         return x[:0]
@@ -196,10 +220,11 @@ def _qr(dev, x, lindep):
     dev.gemm(0, 1, k, k, dim, 1.0, q, dim, q, dim, 0.0, g2, k)
     g2h = g2.cpu().numpy()
     try:
-        low = np.linalg.cholesky(0.5 * (g2h + g2h.T))
+        with _one_blas_thread():
+            low = np.linalg.cholesky(0.5 * (g2h + g2h.T))
+            linv = scipy.linalg.solve_triangular(low, np.eye(k), lower=True)
     except np.linalg.LinAlgError:
         return _qr_vectorwise(dev, x, lindep)
-    linv = scipy.linalg.solve_triangular(low, np.eye(k), lower=True)
     lt = torch.as_tensor(np.ascontiguousarray(linv), device=dev.device)
     out = torch.empty_like(q)
     dev.gemm(0, 0, k, dim, k, 1.0, lt, k, q, dim, 0.0, out, dim)
@@ -242,13 +267,11 @@ def restart_guess(path: str):
 def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e-14,
               max_memory=4000, dot=None, callback=None, nroots=1, lessio=False, pick=None,
               verbose=None, follow_state=False, tol_residual=None, fill_heff=None, device=0,
-              return_device=False, lockstep=None):
-    """lockstep: None -- check the ranks' decisions whenever a process group of size > 1
-    is initialised; True / False to force."""
-    from .parallel import group_size, lockstep_check
+              return_device=False, lockstep=False, group=None):
+    """lockstep: compare every iteration's decisions across the ranks of ``group`` (the
+    replicated solver of a sharded operator); off for an unsharded solve."""
+    from .parallel import lockstep_check
     torch = _torch()
-    if lockstep is None:
-        lockstep = group_size() > 1
     if not torch.cuda.is_available():
         raise RuntimeError("xtddft_amd.davidson1 runs on the GPU; no device is visible")
     dev = _Dev(device)
@@ -281,6 +304,7 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
     conv = np.zeros(nroots, dtype=bool)
     space = 0
     xt = None
+    xt_gram = None          # host Gram matrix of xt, from _normalize_xt_'s round trip
     icyc = 0
     x0r = None
     max_dx_last = 1e9
@@ -294,7 +318,7 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
             x0 = None
             max_dx_last = 1e9            # Davidson.py:168
         elif xt.shape[0] > 1:
-            xt = _qr(dev, xt, lindep)[:40]
+            xt = _qr(dev, xt, lindep, gram=xt_gram)[:40]
         axt = aop(xt)
         if not (hasattr(axt, "is_cuda") and axt.is_cuda):
             axt = torch.as_tensor(np.asarray(axt, dtype=np.float64), device=dev.device)
@@ -314,7 +338,8 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
             heff[i, :i + 1] = hh[ip, :i + 1]
             heff[:i + 1, i] = hh[ip, :i + 1]
         xt = axt = None
-        w, vv = scipy.linalg.eigh(heff[:space, :space])
+        with _one_blas_thread():
+            w, vv = scipy.linalg.eigh(heff[:space, :space])
         if callable(pick):
             w, vv, idx = pick(w, vv, nroots, locals())
             if len(w) == 0:
@@ -341,7 +366,7 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
             conv[k] = abs(de[k]) < tol and dx_norm[k] < toloose
         if lockstep:   # every break / restart decision below follows from these
             lockstep_check(np.concatenate([[icyc, space, nnew, float(np.sum(heff[:space, :space]))],
-                                           e, dx_norm, conv]), f"iteration {icyc}")
+                                           e, dx_norm, conv]), f"iteration {icyc}", group)
         log.debug("davidson %d %d |r|=%.3g e=%s max|de|=%.3g", icyc, space, dx_norm.max(), e,
                   np.abs(de).max())
         if all(conv):
@@ -366,19 +391,25 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
                 x0h = x0r[keep].cpu().numpy()
                 host = np.asarray([precond(host[j], e[0], x0h[j]) for j in range(len(keep))])
                 rk = torch.as_tensor(host, device=dev.device)
-            nrm = np.sqrt(dev.norms2(rk).cpu().numpy())
-            dev.scale_rows(rk, 1.0 / nrm)
-            # _normalize_xt_: project out xs, drop if norm**2 <= lindep, normalise
+            rk = rk * torch.rsqrt(dev.norms2(rk))[:, None]          # normalise on the device
+            # _normalize_xt_: project out xs, drop if norm**2 <= lindep, normalise; the Gram
+            # matrix of the block gives the norms and seeds the next _qr in one round trip
             dev.project_out(rk, xs[:space], space)
-            nrm = np.sqrt(dev.norms2(rk).cpu().numpy())
-            ok = nrm ** 2 > lindep
-            rk = rk[torch.as_tensor(np.where(ok)[0], device=dev.device)].contiguous()
-            dev.scale_rows(rk, 1.0 / nrm[ok])
+            nk = rk.shape[0]
+            g = torch.empty((nk, nk), dtype=torch.float64, device=dev.device)
+            dev.gemm(0, 1, nk, nk, dim, 1.0, rk, dim, rk, dim, 0.0, g, nk)
+            gh = g.cpu().numpy()
+            nrm2 = np.diag(gh).copy()
+            ok = np.where(nrm2 > lindep)[0]
+            sc = 1.0 / np.sqrt(nrm2[ok])
+            rk = rk[torch.as_tensor(ok, device=dev.device)].contiguous()
+            dev.scale_rows(rk, sc)
+            xt_gram = gh[np.ix_(ok, ok)] * sc[:, None] * sc[None, :]
             xt = rk
         else:
             xt = torch.empty((0, dim), dtype=torch.float64, device=dev.device)
         if lockstep:
-            lockstep_check([icyc, xt.shape[0]], f"iteration {icyc} new vectors")
+            lockstep_check([icyc, xt.shape[0]], f"iteration {icyc} new vectors", group)
         if xt.shape[0] == 0:
             conv = dx_norm < toloose
             break

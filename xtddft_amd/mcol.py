@@ -66,9 +66,11 @@ def sf_mc_kernel(mf, collinear_samples: int = 60, device=None, max_points: int =
     """The multicollinear kernel fxc_sf (nk, nk, ngrid) of mean field ``mf``.
 
     ``mf.fxc_sf_mc`` when set (synthetic problems); otherwise computed from the SCF
-    density (or the given spin densities ``rho`` (2, nk, ngrid)) and cached in
-    ``mf.extra`` per sample count.  Returns a host array, or a device tensor when the
-    grid's AO values live in HBM.
+    density and cached in ``mf.extra`` per sample count and orbital set (the cache is
+    keyed on the identity of ``mo_coeff`` / ``mo_occ``: a mean field copied with new
+    orbitals shares ``extra`` but not the kernel), or from the given spin densities
+    ``rho`` (2, nk, ngrid), never cached.  Returns a host array, or a device tensor when
+    the grid's AO values live in HBM.
     """
     import torch
     from .qc import xc as _xc
@@ -77,7 +79,9 @@ def sf_mc_kernel(mf, collinear_samples: int = 60, device=None, max_points: int =
     if mf.xctype == "HF":
         return None
     key = ("fxc_sf_mc", int(collinear_samples))
-    if key in mf.extra and rho is None:
+    ident = (id(mf.mo_coeff), id(mf.mo_occ))
+    cache = rho is None
+    if cache and key in mf.extra and mf.extra.get(key + ("orbitals",)) == ident:
         return mf.extra[key]
     dev = _torch_device(mf, device)
     rho = ground_state_rho(mf, dev) if rho is None else torch.as_tensor(rho, device=dev)
@@ -106,5 +110,7 @@ def sf_mc_kernel(mf, collinear_samples: int = 60, device=None, max_points: int =
     out = 0.5 * (out + out.transpose(0, 1))      # exact symmetry (the (t, s) rotation's round-off)
     ao = mf.grids.ao
     res = out if (isinstance(ao, torch.Tensor) and ao.is_cuda) else out.cpu().numpy()
-    mf.extra[key] = res
+    if cache:
+        mf.extra[key] = res
+        mf.extra[key + ("orbitals",)] = ident
     return res

@@ -74,7 +74,8 @@ class DeviceOperator:
     def __init__(self, mf: MeanField, kind: str, *, sa: int = 0, foo: float = 1.0,
                  fglobal: float = 0.0, remove: bool = False, shard=(0, 1), device: int = 0,
                  stream=None, presharded=False, k_mode: str = "auto",
-                 k_max_gib: float = 0.0, replicate_df=None, sf_kernel: str = "alda0", mc_kernel=None):
+                 k_max_gib: float = 0.0, replicate_df=None, sf_kernel: str = "alda0", mc_kernel=None,
+                 group=None):
         """sf_kernel: spin-flip XC kernel of the SF / XSF kinds -- 'alda0' (method 0,
         mf.fxc_sf) or 'mc' (method 1: the multicollinear kernel ``mc_kernel`` (nk, nk, ngrid),
         ``xtddft_amd.mcol.sf_mc_kernel``).
@@ -85,8 +86,9 @@ class DeviceOperator:
         replicate_df: keep the whole factor on every rank and partition by aux
         window + exchange rows (default: k_mode != 'direct').  With replicate_df, k_mode
         'auto' and an initialised process group, construction is a collective: the ranks
-        agree on stored vs direct exchange (the minimum of their fits), so every rank of
-        the group must construct its operator."""
+        agree on stored vs direct exchange (the minimum of their fits over ``group``, default
+        the WORLD group), so every rank of that group must construct its operator; an
+        operator without an exchange matrix to store skips the agreement."""
         L = _capi.lib()
         self.mf, self.kind = mf, kind
         if sf_kernel not in _capi.SF_KERNEL:
@@ -149,10 +151,11 @@ class DeviceOperator:
             # direct aux window on another do not sum to the operator
             fits, gib = ctypes.c_int(), ctypes.c_double()
             _capi.check(L.xt_exchange_plan(h, ctypes.byref(fits), ctypes.byref(gib)), "xt_exchange_plan")
-            from .parallel import agree_min
-            k_mode = "stored" if agree_min(fits.value) else "direct"
-            _capi.check(L.xt_set_exchange_mode(h, _capi.K_MODE[k_mode], float(k_max_gib)),
-                        "xt_set_exchange_mode")
+            if gib.value > 0:    # same descriptors on every rank: all skip or none does
+                from .parallel import agree_min
+                k_mode = "stored" if agree_min(fits.value, group, device=self.device) else "direct"
+                _capi.check(L.xt_set_exchange_mode(h, _capi.K_MODE[k_mode], float(k_max_gib)),
+                            "xt_set_exchange_mode")
         self.prepare()
         self.setup_s["prepare"] = self.prepare_s
 

@@ -68,19 +68,20 @@ def allreduce_sigma(sigma, group=None):
     return sigma
 
 
-def agree_min(value: int, group=None) -> int:
+def agree_min(value: int, group=None, device=None) -> int:
     """The minimum of an integer decision over the process group (the value itself
     outside a multi-rank group).  Used where a rank-local resolution must be made
     collectively, e.g. whether the stored exchange fits (DeviceOperator): ranks that
     stream stored exchange ROWS and ranks that contract an aux WINDOW directly would
-    not sum to the operator."""
+    not sum to the operator.  ``device``: the GPU of the caller's operator (RCCL reduces
+    device tensors; default the current device)."""
     import torch
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1):
         return int(value)
     t = torch.tensor([int(value)], dtype=torch.int64)
     if dist.get_backend(group) == "nccl":
-        t = t.to(f"cuda:{torch.cuda.current_device()}")
+        t = t.to(f"cuda:{torch.cuda.current_device() if device is None else int(device)}")
     dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
     return int(t.item())
 

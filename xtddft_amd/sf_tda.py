@@ -127,7 +127,8 @@ def davidson_process(mf, nstates, method, isf=-1, device=0, shard=(0, 1), return
                                        collinear_samples=collinear_samples)
     x0 = init_guess(mf, nstates, isf)
     conv, e, x1, icyc = _dav.davidson1(vind, x0, hdiag, tol=1e-7, lindep=1e-14, nroots=nstates,
-                                       max_cycle=3000, device=device)
+                                       max_cycle=3000, device=device,
+                                       lockstep=shard[1] > 1)
     v = np.array(x1).T
     if isf == -1:   # SF_TDA.py:400-401
         v = deal_v_davidson(mf, v)

@@ -260,7 +260,7 @@ class XSF_TDA:
         x0 = self.init_guess(self.nstates, hdiag)
         self.converged, self.e, x1, self.icyc = _dav.davidson1(
             vind, x0, hdiag, tol=1e-8, lindep=1e-9, nroots=self.nstates, max_cycle=1000,
-            device=self.device)
+            device=self.device, lockstep=self.shard[1] > 1)
         self.v = np.array(x1).T
 
     def deltaS2_U(self, nstate):

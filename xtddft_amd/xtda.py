@@ -132,7 +132,8 @@ class XTDA:
             x0 = self.get_init_guess(self.mf, nstates)
         self.converged, self.e, x1, self.icyc = _dav.davidson1(
             vind, x0, precond, tol_residual=self.conv_tol, lindep=self.lindep, nroots=nstates,
-            pick=pickeig, max_cycle=self.max_cycle, device=self.device, callback=self.callback)
+            pick=pickeig, max_cycle=self.max_cycle, device=self.device, callback=self.callback,
+            lockstep=self.shard[1] > 1)
         info = self.mf.shape_info()
         nc, no, nv = info['nc'], info['no'], info['nv']
         v = np.asarray(x1).T
