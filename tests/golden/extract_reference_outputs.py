@@ -21,7 +21,8 @@ Sources (PySCF 2.12.1 / libxc 7.0.0 runs recorded by the reference authors):
   triplet SCF energy.
 * ``example/TDA.ipynb`` (PySCF 2.11.0 / libxc 7.0.0), B3LYP / cc-pVDZ,
   conv_tol 1e-11: cell 2 -- N2 RKS (shell / primitive / AO counts, nuclear
-  repulsion, total grid count, SCF energy, closed-shell TDA singlet roots);
+  repulsion, total grid count, SCF energy, closed-shell TDA singlet roots: the
+  4-decimal table and the 5-decimal "Excited state N  x eV" lines of tda.analyze());
   cell 4 -- CH2O+ (``atom.ch2o_vacuum``) UKS: SCF energy and the U-TDA table
   (energy eV, oscillator strength, Delta<S^2>, 12 roots); cell 6 -- the same
   cation with ROKS: SCF energy and the X-TDA table (``XTDA.kernel``, the
@@ -121,6 +122,9 @@ def main():
             rows.append([float(x) for x in f[1:]])
         rows = np.array(rows)
         out[f"{tag}_td_ev"] = rows[:, 0].tolist()
+        if cell == 2:   # TDA.analyze prints every root again with 5 decimals (TDA.py:283)
+            out[f"{tag}_td_ev5"] = [float(x) for x in re.findall(r"Excited state\s+\d+\s+([-\d.]+) eV", log)]
+            assert len(out[f"{tag}_td_ev5"]) == 12
         out[f"{tag}_td_osc"] = rows[:, 2].tolist()
         if rows.shape[1] > 4:
             out[f"{tag}_td_delta_s2"] = rows[:, 4].tolist()

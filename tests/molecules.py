@@ -136,6 +136,27 @@ def tda_meanfield(name: str):
     return tda_scf(name).to_meanfield()
 
 
+def closed_shell_singlets(mf, w, v):
+    """Singlet eigenvalues of a U-TDA matrix on a closed-shell UKS mean field.
+
+    Eigenvectors (columns of v, PySCF order [za | zb]) are singlets when za equals zb
+    once zb is expressed in the alpha MOs -- the alpha and beta orbitals of a UKS
+    solution agree only up to signs and rotations among degenerate orbitals, so the
+    beta block is rotated by the MO overlap O = C_a^T S C_b first (TDA.py's singlet
+    A = Delta eps + 2 (ia|jb) - c_x (ij|ab) + 2 f_xc is the za = zb block)."""
+    import numpy as np
+    info = mf.shape_info()
+    no, nv = info["nocc_a"], info["nvir_a"]
+    ca, cb = mf.mo_coeff
+    o = ca.T @ mf.extra["s1e"] @ cb
+    n = no * nv
+    za = v[:n].T.reshape(-1, no, nv)
+    zb = np.einsum('ij,kjb,ab->kia', o[:no, :no], v[n:].T.reshape(-1, no, nv), o[no:, no:])
+    cos = np.einsum('kia,kia->k', za, zb) / np.sqrt(np.einsum('kia,kia->k', za, za)
+                                                     * np.einsum('kia,kia->k', zb, zb))
+    return np.asarray(w)[cos > 0.5]
+
+
 def analyze_mismatch(x, ref_states, tol=2e-4):
     """Largest deviation between XTDA.analyze()'s spin-tensor coefficients (so2st of the
     solver's eigenvectors, XTDA.py:893-937) and the reference's printed ones, in magnitude:

@@ -4,7 +4,9 @@ HF molecule / 6-31G / BHandHLYP (``example/XSF_TDA.ipynb``): the SCF runs on the
 host (``xtddft_amd.qc``), the TDA operators and the Davidson solver run on the
 MI355X through the C ABI -- in jk_mode DF (exact Cholesky factor of the ERIs)
 and in jk_mode ERI8 (the device factorises the stored 8-fold ERIs itself).
-Tolerance: 1e-6 Ha on excitation energies (BASELINE.json north_star).
+Tolerance: 1e-7 Ha on the notebook's 8-decimal XSF / USF roots (BASELINE.json north_star
+asks for 1e-6; the oracle itself agrees with them to 4.3e-8), 1e-5 eV (3.7e-7 Ha) on the
+5-decimal N2 singlets.
 """
 import numpy as np
 import pytest
@@ -17,7 +19,7 @@ from xtddft_amd.utils import HA2EV
 
 pytestmark = pytest.mark.gpu
 
-TOL_HA = 1e-6
+TOL_HA = 1e-7
 
 
 @pytest.fixture(scope="module")
@@ -215,6 +217,22 @@ def test_utda_closed_shell_n2_contains_reference_tda_singlets(torch):
     w = np.linalg.eigvalsh(x.A) * HA2EV
     for e in reference_outputs()["n2_rks_b3lyp_td_ev"]:
         assert np.abs(w - e).min() < 6e-5, e
+
+
+def test_utda_closed_shell_n2_singlets_match_five_decimal_printout(torch):
+    """The same N2 operator (device explicit A) against the 5-decimal "Excited state"
+    lines of the notebook (TDA.py:283): the singlet eigenvalues, in order, to 1e-5 eV."""
+    from molecules import closed_shell_singlets, tda_meanfield
+    from xtddft_amd import XTDA
+    mf = tda_meanfield("N2_UKS")
+    x = XTDA(mf.mol, mf, nstates=60, use_Davidson=False)
+    x.kernel()
+    inv = np.argsort(x.order)                  # x.A is in "my order" (XTDA.py:799-800)
+    a = x.A[np.ix_(inv, inv)]
+    w, v = np.linalg.eigh(0.5 * (a + a.T))
+    s = closed_shell_singlets(mf, w, v)[:12] * HA2EV
+    ref = np.asarray(reference_outputs()["n2_rks_b3lyp_td_ev5"])
+    assert np.abs(s - ref).max() < 1e-5, (s, ref)
 
 
 def test_sf_up_on_aufbau_triplet_matches_oracle(torch):

@@ -202,6 +202,24 @@ def test_oracle_utda_on_closed_shell_contains_tda_singlets():
         assert np.abs(w - e).min() < TD_PRINT_TOL_EV, e
 
 
+def test_oracle_closed_shell_singlets_match_five_decimal_printout():
+    """N2 / B3LYP / cc-pVDZ: the 12 singlet roots tda.analyze() printed with 5 decimals
+    (example/TDA.ipynb cell 2, TDA.py:283) against the singlet eigenvalues of the oracle's
+    U-TDA matrix on the closed-shell UKS mean field, in order, to 1e-5 eV (~3.7e-7 Ha; the
+    print rounds to 5e-6 eV; the reference's TDA.py diagonalises its explicit A, no
+    solver tolerance)."""
+    from molecules import closed_shell_singlets, tda_meanfield
+    from oracle import xtda as oxtda
+    from xtddft_amd.utils import HA2EV
+    mf = tda_meanfield("N2_UKS")
+    vind, hdiag = oxtda.gen_tda_operation(mf)
+    a = vind(np.eye(hdiag.size)).T
+    w, v = np.linalg.eigh(0.5 * (a + a.T))
+    s = closed_shell_singlets(mf, w, v)[:12] * HA2EV
+    ref = np.asarray(reference_outputs()["n2_rks_b3lyp_td_ev5"])
+    assert np.abs(s - ref).max() < 1e-5, (s, ref)
+
+
 def test_roks_orbital_energies_match_reference():
     """Roothaan orbital energies; the reference printed them one cycle before the
     final one (|ddm| ~ 3e-5 there), hence the looser tolerance."""
