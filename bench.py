@@ -466,9 +466,10 @@ def converge(args, w, allreduce, world=1):
               return_device=True, lockstep=world > 1, **warm)
     torch.cuda.synchronize()
     log(f"converging {args.nroots} roots")
+    phase_s = {}
     tc = time.perf_counter()
     conv, e, _, icyc = davidson1(aop, x0, pre, nroots=args.nroots, device=dev.index,
-                                 return_device=True, lockstep=world > 1, **kw)
+                                 return_device=True, lockstep=world > 1, stats=phase_s, **kw)
     torch.cuda.synchronize()
     wall = time.perf_counter() - tc
     hist = {}
@@ -480,6 +481,7 @@ def converge(args, w, allreduce, world=1):
                 converged=bool(np.all(conv)), ax_calls=stats["calls"], ax_vectors=stats["vectors"],
                 ax_s=round(stats["s"], 3), allreduce_s=round(stats["allreduce_s"], 3),
                 host_davidson_s=round(host, 4), host_ms_per_iteration=round(1e3 * host / (int(icyc) + 1), 3),
+                solver_phase_ms={k: round(1e3 * v, 2) for k, v in phase_s.items()},
                 nvec_histogram={str(k): v for k, v in sorted(hist.items())},
                 e_min_ha=float(e[0]), e_ha=[float(v) for v in e], criteria=crit,
                 warmup="an untimed 2-iteration solve first (solver kernels loaded)")

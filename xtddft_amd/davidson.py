@@ -145,11 +145,12 @@ def _gram_gs(g, lindep):
     """Gram-Schmidt in coefficient space: rows of C (kept x n) with C x
     orthonormal, processing the rows of x in order and dropping a row whose
     residual norm**2 <= lindep (PySCF _qr's rule) -- from the Gram matrix
-    g = x x^T alone.  Returns (C, smallest kept norm**2)."""
+    g = x x^T alone.  Returns (C, smallest kept norm**2, smallest kept norm**2 relative to
+    the row's own norm**2)."""
     n = g.shape[0]
     c = np.zeros((n, n))
     kept = 0
-    nmin = np.inf
+    nmin = rmin = np.inf
     for i in range(n):
         r = np.zeros(n)
         r[i] = 1.0
@@ -161,12 +162,17 @@ def _gram_gs(g, lindep):
             c[kept] = r / np.sqrt(nrm2)
             kept += 1
             nmin = min(nmin, nrm2)
-    return c[:kept], nmin
+            rmin = min(rmin, nrm2 / g[i, i])
+    return c[:kept], nmin, rmin
 
 
 # Below this residual norm**2 the Gram-matrix route loses the accuracy the drop rule
 # needs (its rounding grows like eps / norm**2): orthonormalise vector by vector instead.
 GRAM_SAFE_NORM2 = 1e-8
+# Above this smallest kept residual norm**2 (relative to the row's norm**2) one Gram-Schmidt
+# pass is orthogonal to ~eps / ratio <= 1e-14 (the reference's one-pass modified Gram-Schmidt is no better): the
+# Cholesky-QR second pass and its host round trip are skipped.
+QR_ONE_PASS_NORM2 = 1e-2
 
 
 def _qr_vectorwise(dev, x, lindep):
@@ -207,7 +213,7 @@ def _qr(dev, x, lindep, gram=None):
         dev.gemm(0, 1, n, n, dim, 1.0, x, dim, x, dim, 0.0, g, n)
         gram = g.cpu().numpy()
     with _one_blas_thread():
-        c, nmin = _gram_gs(gram, lindep)
+        c, nmin, rmin = _gram_gs(gram, lindep)
     k = c.shape[0]
     if k == 0:
         return x[:0]
@@ -216,6 +222,8 @@ def _qr(dev, x, lindep, gram=None):
     ct = torch.as_tensor(np.ascontiguousarray(c), device=dev.device)
     q = torch.empty((k, dim), dtype=torch.float64, device=dev.device)
     dev.gemm(0, 0, k, dim, n, 1.0, ct, n, x, dim, 0.0, q, dim)
+    if rmin > QR_ONE_PASS_NORM2:
+        return q
     g2 = torch.empty((k, k), dtype=torch.float64, device=dev.device)
     dev.gemm(0, 1, k, k, dim, 1.0, q, dim, q, dim, 0.0, g2, k)
     g2h = g2.cpu().numpy()
@@ -267,11 +275,22 @@ def restart_guess(path: str):
 def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e-14,
               max_memory=4000, dot=None, callback=None, nroots=1, lessio=False, pick=None,
               verbose=None, follow_state=False, tol_residual=None, fill_heff=None, device=0,
-              return_device=False, lockstep=False, group=None):
+              return_device=False, lockstep=False, group=None, stats=None):
     """lockstep: compare every iteration's decisions across the ranks of ``group`` (the
-    replicated solver of a sharded operator); off for an unsharded solve."""
+    replicated solver of a sharded operator); off for an unsharded solve.
+    stats: a dict that receives the wall seconds per solver phase (qr, aop, heff, eigh,
+    ritz, lockstep, precond, other) -- the phases end at host round trips, so no
+    synchronisation is added."""
+    import time
     from .parallel import lockstep_check
     torch = _torch()
+    t_last = [time.perf_counter()]
+
+    def tick(name):
+        if stats is not None:
+            t = time.perf_counter()
+            stats[name] = stats.get(name, 0.0) + t - t_last[0]
+            t_last[0] = t
     if not torch.cuda.is_available():
         raise RuntimeError("xtddft_amd.davidson1 runs on the GPU; no device is visible")
     dev = _Dev(device)
@@ -319,9 +338,11 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
             max_dx_last = 1e9            # Davidson.py:168
         elif xt.shape[0] > 1:
             xt = _qr(dev, xt, lindep, gram=xt_gram)[:40]
+        tick("qr")
         axt = aop(xt)
         if not (hasattr(axt, "is_cuda") and axt.is_cuda):
             axt = torch.as_tensor(np.asarray(axt, dtype=np.float64), device=dev.device)
+        tick("aop")
         nnew = xt.shape[0]
         if space + nnew > cap:
             raise RuntimeError("Davidson subspace overflow")
@@ -338,8 +359,10 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
             heff[i, :i + 1] = hh[ip, :i + 1]
             heff[:i + 1, i] = hh[ip, :i + 1]
         xt = axt = None
+        tick("heff")
         with _one_blas_thread():
             w, vv = scipy.linalg.eigh(heff[:space, :space])
+        tick("eigh")
         if callable(pick):
             w, vv, idx = pick(w, vv, nroots, locals())
             if len(w) == 0:
@@ -351,8 +374,9 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
             elast, conv_last = _sort_elast(elast, conv_last, vlast, v)
         de = e if (elast is None or elast.size != e.size) else e - elast
         nr = e.size
-        vt = torch.as_tensor(np.ascontiguousarray(v.T), device=dev.device)         # (nr, space)
-        vte = torch.as_tensor(np.ascontiguousarray(-(v * e).T), device=dev.device)
+        # v^T and -(v e)^T in one upload
+        vv2 = torch.as_tensor(np.ascontiguousarray(np.concatenate([v.T, -(v * e).T])), device=dev.device)
+        vt, vte = vv2[:nr], vv2[nr:]                                                # (nr, space) each
         x0r = torch.empty((nr, dim), dtype=torch.float64, device=dev.device)
         dev.gemm(0, 0, nr, dim, space, 1.0, vt, space, xs, dim, 0.0, x0r, dim)     # x0 = v^T xs
         # ax0 = v^T ax.  (lessio recomputes A x0 only when the subspace is not held
@@ -364,9 +388,11 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
         dx_norm = np.sqrt(dev.norms2(r).cpu().numpy())
         for k in range(nr):
             conv[k] = abs(de[k]) < tol and dx_norm[k] < toloose
+        tick("ritz")
         if lockstep:   # every break / restart decision below follows from these
             lockstep_check(np.concatenate([[icyc, space, nnew, float(np.sum(heff[:space, :space]))],
                                            e, dx_norm, conv]), f"iteration {icyc}", group)
+        tick("lockstep")
         log.debug("davidson %d %d |r|=%.3g e=%s max|de|=%.3g", icyc, space, dx_norm.max(), e,
                   np.abs(de).max())
         if all(conv):
@@ -408,6 +434,7 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
             xt = rk
         else:
             xt = torch.empty((0, dim), dtype=torch.float64, device=dev.device)
+        tick("precond")
         if lockstep:
             lockstep_check([icyc, xt.shape[0]], f"iteration {icyc} new vectors", group)
         if xt.shape[0] == 0:
@@ -419,6 +446,7 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
             x0 = x0r
         if callable(callback):
             callback(locals())
+        tick("other")
     if return_device:
         return np.asarray(conv), e, x0r, icyc
     x_host = x0r.cpu().numpy()
