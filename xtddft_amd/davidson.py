@@ -28,12 +28,13 @@ across the ranks of ``group`` (``parallel.lockstep_check``): a divergence raises
 ranks instead of leaving some waiting in the next all-reduce.  An unsharded solve
 never communicates, whatever process group exists.
 
-Host cost per iteration (the part that does not shrink with more GPUs): four device ->
+Host cost per iteration (the part that does not shrink with more GPUs): three device ->
 host round trips (heff rows, residual norms, the Gram matrix of the new block -- its
-diagonal is the drop test of ``_normalize_xt_`` and it seeds the next ``_qr`` -- and the
-Cholesky-QR pass), and the small host LAPACK (heff ``eigh``, the coefficient-space
-Gram-Schmidt) on one BLAS thread: a multithreaded BLAS is slower on matrices of this
-size (measured: eigh of 70 x 70 at 0.6 ms on one thread, up to 8 ms on eight).  ``precond``
+diagonal is the drop test of ``_normalize_xt_`` and it seeds the next ``_qr``; a fourth,
+the Cholesky-QR pass, only for nearly dependent blocks), and the small host LAPACK (heff
+``eigh`` by divide and conquer, the coefficient-space Gram-Schmidt) on one BLAS thread: a
+multithreaded BLAS is slower on matrices of this size (measured: eigh of 70 x 70 at 0.6 ms
+on one thread, up to 8 ms on eight).  ``stats`` returns the per-phase split.  ``precond``
 may be a diagonal (array or device tensor: PySCF ``make_diag_precond`` with
 level shift 1e-3), a ``DiagPrecond`` (device kernel), or any host callable
 ``precond(dx, e, x0)`` (evaluated on host copies).
@@ -360,8 +361,8 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
             heff[:i + 1, i] = hh[ip, :i + 1]
         xt = axt = None
         tick("heff")
-        with _one_blas_thread():
-            w, vv = scipy.linalg.eigh(heff[:space, :space])
+        with _one_blas_thread():     # divide and conquer: the fastest LAPACK driver at these sizes
+            w, vv = scipy.linalg.eigh(heff[:space, :space], driver="evd")
         tick("eigh")
         if callable(pick):
             w, vv, idx = pick(w, vv, nroots, locals())
@@ -428,8 +429,11 @@ def davidson1(aop, x0, precond, tol=1e-12, max_cycle=50, max_space=12, lindep=1e
             nrm2 = np.diag(gh).copy()
             ok = np.where(nrm2 > lindep)[0]
             sc = 1.0 / np.sqrt(nrm2[ok])
-            rk = rk[torch.as_tensor(ok, device=dev.device)].contiguous()
-            dev.scale_rows(rk, sc)
+            if ok.size == nk:        # nothing dropped: scale by the device copy of the diagonal
+                rk = rk * torch.rsqrt(torch.diagonal(g))[:, None]
+            else:
+                rk = rk[torch.as_tensor(ok, device=dev.device)].contiguous()
+                dev.scale_rows(rk, sc)
             xt_gram = gh[np.ix_(ok, ok)] * sc[:, None] * sc[None, :]
             xt = rk
         else:
