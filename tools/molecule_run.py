@@ -269,7 +269,8 @@ def main():
         # the grid AO values stay in HBM for large molecules: the oracle reads them block by block
         ao = mfield.grids.ao
         if big and hasattr(ao, "cpu"):
-            ao = _DevSlicer(ao[:1] if a.kind != "xtda" else ao)
+            # ALDA0 spin flip reads AO values only; X-TDA and the multicollinear kernel need gradients
+            ao = _DevSlicer(ao[:1] if (a.kind != "xtda" and a.method == 0) else ao)
         else:
             ao = _host(ao)
         mfo = dataclasses.replace(mfield, cderi=_host(mfield.cderi),

@@ -111,6 +111,23 @@ class DeviceEngine:
         return np.stack([self._k(d.reshape(-1, self.n, self.n)[x], dt[x], B) for x in range(dt.shape[0])]
                         ).reshape(d.shape)
 
+    def _reduce_p(self, t, b, nt):
+        """sum_P op(t_P) b_P for slabs t (P, n, k) and b (P, k, n) or, with nt, b (P, n, k)
+        transposed: one engine GEMM whose reduce index is P (``xt_dgemm_strided``) --
+        no (n, P k) re-layout copy, and no row stride P k (which the engine's 32-bit
+        tile addressing caps near 2M at large aux counts)."""
+        torch = self.torch
+        P, m, k = t.shape
+        n = b.shape[1] if nt else b.shape[2]
+        c = torch.empty((m, n), dtype=torch.float64, device=self.dev)
+        sbk, sbn = (1, k) if nt else (n, 1)
+        st = torch.cuda.current_stream(self.dev).cuda_stream
+        with torch.cuda.device(self.dev):
+            _capi.check(self.L.xt_dgemm_strided(m, n, k, P, 1, 1.0, t.data_ptr(), k, 1, m * k, 0,
+                                                b.data_ptr(), sbk, sbn, b.shape[1] * b.shape[2], 0, 0.0,
+                                                c.data_ptr(), n, 0, ctypes.c_void_p(st)), "xt_dgemm_strided")
+        return c
+
     def _k(self, dh, dd, B=None):
         """K[D] (host array) for one density (dh host, dd the same on the device)."""
         torch = self.torch
@@ -123,11 +140,11 @@ class DeviceEngine:
             if r == 0:
                 return np.zeros((n, n))
             vt = torch.as_tensor(np.ascontiguousarray(v[:, keep]), device=self.dev)
-            t = self._mm(B.reshape(P * n, n), vt).reshape(P, n, r).permute(1, 0, 2).contiguous()
+            t = self._mm(B.reshape(P * n, n), vt).reshape(P, n, r)       # T_P = B_P V
             ts = t * torch.as_tensor(lam[keep], device=self.dev)
-            return self._mm(t.reshape(n, P * r), ts.reshape(n, P * r), tb=1).cpu().numpy()
-        t = self._mm(B.reshape(P * n, n), dd).reshape(P, n, n).permute(1, 0, 2).contiguous()
-        return self._mm(t.reshape(n, P * n), B.reshape(P * n, n)).cpu().numpy()
+            return self._reduce_p(t, ts, nt=True).cpu().numpy()          # sum_P T_P lam T_P^T
+        t = self._mm(B.reshape(P * n, n), dd).reshape(P, n, n)           # B_P D
+        return self._reduce_p(t, B, nt=False).cpu().numpy()              # sum_P B_P D B_P
 
     # ------------------------------------------------------------ XC
     def _rho(self, dm):
