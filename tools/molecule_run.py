@@ -106,7 +106,7 @@ MOLECULES = {
                       kind="sfup", xc="bhandhlyp", tol=1e-8,
                       label="free-base porphyrin triplet / cc-pVDZ (atom.py:313; BASELINE C3 class: SF-up)"),
     "c60-": dict(atom=None, basis="cc-pvdz", charge=-1, spin=1, nroots=40, kind="xsf", sa=0,
-                 xc="bhandhlyp", tol=1e-6,
+                 xc="bhandhlyp", tol=1e-8,
                  label="C60- doublet / cc-pVDZ (nao 840 = BASELINE C4's; XSF-TDA SA = 0, C4d's kind)"),
 }
 

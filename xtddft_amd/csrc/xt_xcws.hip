@@ -41,7 +41,12 @@ constexpr int SW_AC = 2 * SW_WA;           // virtuals per staged chunk
 constexpr int SW_WP = SW_AC + 2;           // weight pitch, 2 mod 32: conflict-free ds_read_b64
 constexpr int SW_PP = 52;                  // PhiO pitch, 4 mod 8: conflict-free ds_read_b128
 constexpr int SW_W_IMG = 3 * SW_GB * SW_WP;
-constexpr size_t SW_LDS = sizeof(double) * ((size_t)SW_GB * SW_PP + SW_W_IMG);
+// The single k-step of an odd KS reads one double per lane (rows 8 KP + q): from the PhiO
+// image (pitch 52, 8 mod 16 in bank pairs) the 16 lanes of a ds_read2 group would hit 4
+// bank pairs 4 times each (measured: 0.41 SQ_LDS_BANK_CONFLICT cycles per LDS instruction
+// at C2, O = 34); those four rows get their own image of odd pitch 5 (16 distinct pairs).
+constexpr int SW_P1 = 5;
+constexpr size_t SW_LDS = sizeof(double) * ((size_t)SW_GB * SW_PP + SW_W_IMG + (size_t)SW_GB * SW_P1);
 constexpr int SW_KS_MAX = 12;              // k-steps: KI = 4 KS <= 48 <= SW_PP
 }  // namespace
 
@@ -61,6 +66,7 @@ k_xc_rho_ws(int O, int nx, int V, int n,
   extern __shared__ __attribute__((aligned(16))) double sm[];
   double* sP = sm;                                   // [GB][PP]
   double* sW = sm + SW_GB * SW_PP;                   // [3][GB][WP]
+  double* sP1 = sW + SW_W_IMG;                       // [GB][P1]: PhiO rows 8 KP .. 8 KP + 3 (odd KS)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -73,7 +79,9 @@ k_xc_rho_ws(int O, int nx, int V, int n,
   // ---- PhiO tile -> LDS, once (rows past O and points past n as zero) ---------------
   for (int p = tid; p < KI * SW_GB; p += NT) {
     const int g = p / KI, i = p % KI;
-    sP[g * SW_PP + i] = (i < O && g0 + g < n) ? PO[(long)(g0 + g) * ldp + i] : 0.0;
+    const double v = (i < O && g0 + g < n) ? PO[(long)(g0 + g) * ldp + i] : 0.0;
+    sP[g * SW_PP + i] = v;
+    if (ODD && i >= 8 * KP) sP1[g * SW_P1 + i - 8 * KP] = v;
   }
 
   // ---- Zp walk: units (chunk, pair, a-tile of the chunk) in order; lane (q, r16) of
@@ -118,9 +126,9 @@ k_xc_rho_ws(int O, int nx, int V, int n,
     for (int j = 0; j < SW_TNG; ++j) dst[j] = src[(16 * j * SW_PP) / 2];
   };
   auto bread1 = [&]() XT_INLINE {
-    const double* src = sP + r16 * SW_PP + 8 * KP + q;
+    const double* src = sP1 + r16 * SW_P1 + q;
 #pragma unroll
-    for (int j = 0; j < SW_TNG; ++j) bs[j] = src[16 * j * SW_PP];
+    for (int j = 0; j < SW_TNG; ++j) bs[j] = src[16 * j * SW_P1];
   };
   auto bfirst = [&]() XT_INLINE {                   // the B operand of a tile's first k-step
     if constexpr (KP > 0) bread(0, bq[0]);
