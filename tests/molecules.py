@@ -35,9 +35,12 @@ def hf_scf(kind: str):
     'ROKS_AUFBAU' = example/spin up.ipynb (H 0 0 0; F 0 0 1.0, no constraint);
     'ROKS_TPSS' / 'UKS_TPSS': the same molecule with the TPSS meta-GGA (unpinned
     energy; the source of the MGGA response checks); 'ROKS_CAMB3LYP' / 'UKS_CAMB3LYP'
-    with the range-separated CAM-B3LYP (unpinned; the long-range exchange checks)."""
-    if kind.endswith("_TPSS") or kind.endswith("_CAMB3LYP"):
-        xc = "tpss" if kind.endswith("_TPSS") else "cam-b3lyp"
+    with the range-separated CAM-B3LYP (unpinned; the long-range exchange checks); '_WB97XD' /
+    '_PBE0' suffixes: omegaB97X-D and PBE0 (the reference's demo functionals, unpinned)."""
+    extra = {"_TPSS": "tpss", "_CAMB3LYP": "cam-b3lyp", "_WB97XD": "wb97x-d", "_PBE0": "pbe0"}
+    suffix = next((k for k in extra if kind.endswith(k)), None)
+    if suffix is not None:
+        xc = extra[suffix]
         mf = (ROKS if kind.startswith("ROKS") else UKS)(hf_mol(), xc)
         mf.irrep_nelec = dict(HF_IRREP_NELEC)
         mf.conv_tol = 1e-11

@@ -684,7 +684,53 @@ def test_camb3lyp_coefficients_and_b88_limit():
     assert float(sr_big.abs().max()) < 1e-6 * float(full.abs().max())
 
 
-@pytest.mark.parametrize("kind", ["ROKS", "UKS"])
+def test_pbe_hydrogen_atom_energies():
+    """PBE exchange and correlation of the exact hydrogen-atom density (fully spin
+    polarised, rho = exp(-2 r) / pi) against Perdew, Burke and Ernzerhof's published values
+    (PRL 77, 3865 (1996), Table I: E_x^LDA -0.2680, E_x^PBE -0.3059, E_c^PBE -0.0060 Ha)."""
+    from numpy.polynomial.legendre import leggauss
+    from xtddft_amd.qc import xc
+    x, w = leggauss(400)
+    r = (1 + x) / (1 - x) * 2.0
+    wr = 4 * np.pi * r * r * w * 4.0 / (1 - x) ** 2
+    rho = np.exp(-2 * r) / np.pi
+    R = np.zeros((2, 4, r.size))
+    R[0, 0], R[0, 3], R[1, 0] = rho, -2 * rho, 1e-300
+
+    def energy(f):
+        return float((wr * xc.eval_xc_eff(f, R, 1)[0] * rho).sum())
+    ex_lda, e_pbe0 = energy("SLATER"), energy("PBE0")
+    e_pbe = energy("PBE")
+    ex_pbe = (e_pbe - e_pbe0) / 0.25          # PBE0 = 0.75 PBE x + PBE c
+    ec_pbe = e_pbe - ex_pbe
+    assert abs(ex_lda + 0.2680) < 5e-5 and abs(ex_pbe + 0.3059) < 5e-5 and abs(ec_pbe + 0.0060) < 5e-5
+    assert xc.rsh_and_hybrid_coeff("PBE0") == (0.0, 0.25, 0.25)
+    assert xc.rsh_and_hybrid_coeff("pbe38") == (0.0, 0.375, 0.375)
+
+
+def test_wb97xd_coefficients_and_limits():
+    """omegaB97X-D: PySCF's (omega, alpha, hyb) = (0.2, 1.0, 0.222036); the uniform-gas limit
+    of its series (s = 0: exchange c_x0 = 1 - 0.222036 times the short-range LSDA exchange,
+    correlation exactly PW92 through the same-spin / opposite-spin split), the omega -> 0
+    limit of the short-range exchange (the unattenuated LSDA) and omega -> infinity (zero)."""
+    import torch
+    from xtddft_amd.qc import xc
+    assert xc.rsh_and_hybrid_coeff("wB97X-D") == (0.2, 1.0, 0.222036)
+    assert abs(xc._WB97XD["cx"][0] + 0.222036 - 1.0) < 1e-12
+    rng = np.random.default_rng(4)
+    t = lambda v: torch.tensor(v, dtype=torch.float64)
+    ra, rb = t(rng.uniform(0.05, 3, 50)), t(rng.uniform(0.05, 3, 50))
+    z = torch.zeros_like(ra)
+    slater = xc._slater(ra, rb, z, z, z, torch)
+    x0 = xc._wb97x_x(ra, rb, z, z, z, torch, 1e-10)
+    assert torch.allclose(x0, 0.777964 * slater, rtol=1e-9)
+    assert float(xc._wb97x_x(ra, rb, z, z, z, torch, 1e5).abs().max()) < 1e-7 * float(slater.abs().max())
+    n = ra + rb
+    pw = n * xc._ec_pw92(n, (ra - rb) / n, torch)
+    assert torch.allclose(xc._wb97x_c(ra, rb, z, z, z, torch), pw, rtol=1e-12)
+
+
+@pytest.mark.parametrize("kind", ["ROKS", "UKS", "ROKS_WB97XD", "UKS_PBE0"])
 def test_camb3lyp_scf_energy_is_stationary(kind):
     """Range-separated SCF (CAM-B3LYP, K = hyb K + (alpha - hyb) K_LR): the energy is the
     functional whose derivative is the Fock matrix -- central differences of
@@ -692,8 +738,10 @@ def test_camb3lyp_scf_energy_is_stationary(kind):
     the long-range exchange's energy factor and potential together; the SCF converges.
     Parity unpinned (no reference printout with a range-separated functional)."""
     from molecules import hf_scf
-    mf = hf_scf(f"{kind}_CAMB3LYP")
-    assert mf.converged and mf.omega == 0.33 and mf.eri_lr is not None
+    mf = hf_scf(kind if "_" in kind else f"{kind}_CAMB3LYP")
+    assert mf.converged
+    if "PBE0" not in kind:
+        assert mf.omega in (0.33, 0.2) and mf.eri_lr is not None
     d0 = np.asarray(mf._dm)
     rng = np.random.default_rng(5)
     dl = rng.normal(size=d0.shape) * 1e-2
@@ -707,6 +755,8 @@ def test_camb3lyp_scf_energy_is_stationary(kind):
     eps = 1e-4
     fd = (etot(d0 + eps * dl) - etot(d0 - eps * dl)) / (2 * eps)
     assert abs(fd - grad) < 1e-7 * max(1.0, abs(grad))
+    if "PBE0" in kind:
+        return
     # the long-range part is really there: K_LR differs from K and from zero
     klr = mf.get_k_lr(d0)
     k = mf.get_jk(dm=d0)[1]

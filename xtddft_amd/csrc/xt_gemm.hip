@@ -17,8 +17,8 @@
 // (BM/WGM)x(BN/WGN) made of 16x16 v_mfma_f64_16x16x4_f64 tiles (configs: kCfg).
 // LDS holds As[m][k] / Bs[n][k] (k contiguous, odd row pitch BK + 1 doubles),
 // double buffered with register staging.  Lane l (q = l>>4) feeds MFMA step s
-// of a K-tile with k = q + 4s (BK 16) or k = koff(q) + s (BK 32, bank-conflict-free
-// fragment reads, see compute) -- the k permutation is applied identically to
+// of a K-tile with k = q + 4s (k = koff(q) + s on the 64 x 64 BK 32 tile: bank-conflict-
+// free fragment reads, see compute) -- the k permutation is applied identically to
 // A and B, so the sum over k is unchanged.  Staging addresses are per-thread
 // 32-bit offsets computed once; the K loop body is branch-free.
 // C/D layout of the f64 MFMA: col = lane & 15, row = (lane >> 4) + 4*reg
@@ -45,7 +45,7 @@ namespace xt {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-// LDS row pitch in doubles (LDP = BK + 1; BK + 2 for the k-contiguous BK 16 tiles, see the kernel).  The compiler pairs the per-step fragment reads into
+// LDS row pitch in doubles (LDP = BK + 1).  The compiler pairs the per-step fragment reads into
 // ds_read2_b64, whose lane groups are 16 lanes over 32 banks: lane (q, r) of a
 // group reads row r at k = q + 4s, i.e. dword 2*(LDP*r + q) mod 32, which is
 // conflict-free for any odd pitch.  Odd pitch also keeps both staging stores
@@ -113,11 +113,9 @@ dgemm_kernel(GemmParams p) {
                 "fused XC modes run on 128-row (mode 2 also 64-row) 8-wave tiles, A MN-contiguous, "
                 "B staged K-contiguous");
   static_assert(MODE != 2 || (WGM == 2 && WGN == 4), "mode 2 staging map assumes 2x4 waves");
-  // BK 16 with both operands k-contiguous (staging stores are runs of consecutive k, any
-  // pitch is conflict-free for them): pitch 18, so the ds_read_b64 fragment reads of lane
-  // rows q = 0, 1 (k = 4 s, 4 s + 1) land on disjoint bank pairs (36 r and 36 r + 2 mod 64);
-  // the odd pitch 17 collides row 15 of q = 1 with row 0 of q = 0 on every read.
-  constexpr int LDP = (MODE == 0 && BK == 16 && A_KC && B_KC) ? BK + 2 : BK + 1;
+  // (Pitch 18 for the k-contiguous BK 16 tiles makes their ds_read_b64 fragment reads
+  // conflict-free but measured slower: C2 forward U 1.71-1.74 -> 1.76 ms, same box.)
+  constexpr int LDP = BK + 1;
   constexpr int NTHREADS = 64 * WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;    // wave tile
   constexpr int TM = WM / 16, TN = WN / 16;      // MFMA tiles per wave
@@ -348,16 +346,19 @@ dgemm_kernel(GemmParams p) {
   // never stored); K_EDGE: skip k-steps wholly past K (their B rows are zero).
   // Fragment reads stay unconditional (LDS holds clamped rows), so the read
   // pipelining is identical in every variant.
-  // Lane row q's k offset inside a K-tile and the k stride between MFMA steps.  BK 16:
-  // k = q + 4 s.  BK 32: k = koff(q) + s with koff = 0, 16, 8, 24 -- the fragment reads the
-  // compiler emits as ds_read_b64 serve lanes 0-31 (q = 0, 1) and 32-63 (q = 2, 3) in one
-  // LDS cycle each over 64 banks: with k = q + 4 s and the odd pitch, lane (r + 1, q = 0)
-  // and lane (r, q = 1) hit the same bank pair (2-way conflict on every read, measured as
-  // one SQ_LDS_BANK_CONFLICT cycle per LDS instruction on C2's back L); 16 doubles apart the
-  // two lane rows use disjoint halves of the banks.  The 16-lane groups of ds_read2_b64 and
-  // the staging stores see only the row stride and stay conflict-free.
-  constexpr int KSTEP = BK == 32 ? 1 : 4;
-  const int koff = BK == 32 ? 16 * (q & 1) + 8 * (q >> 1) : q;
+  // Lane row q's k offset inside a K-tile and the k stride between MFMA steps: k = q + 4 s,
+  // except on the 64 x 64 BK 32 tile, k = koff(q) + s with koff = 0, 16, 8, 24.  The fragment
+  // reads the compiler emits as ds_read_b64 serve lanes 0-31 (q = 0, 1) and 32-63 (q = 2, 3)
+  // in one LDS cycle each over 64 banks: with k = q + 4 s and the odd pitch, lane (r + 1,
+  // q = 0) and lane (r, q = 1) hit the same bank pair (a 2-way conflict on every read: one
+  // SQ_LDS_BANK_CONFLICT cycle per LDS instruction on C2's back L, which runs this tile);
+  // 16 doubles apart the two lane rows use disjoint halves of the banks (C2 back L: 0
+  // conflicts, 2.15-2.19 -> 2.11-2.15 ms same box).  On the 128 x 128 BK 32 tile the same
+  // permutation removes the conflicts but measured slower (headline back L 141.0-141.3 ->
+  // 143.9-144.1 ms per step, same box): not applied there.
+  constexpr bool KPERM = BK == 32 && BM == 64 && BN == 64;
+  constexpr int KSTEP = KPERM ? 1 : 4;
+  const int koff = KPERM ? 16 * (q & 1) + 8 * (q >> 1) : q;
   auto compute = [&](int buf, auto MN_EDGE, auto K_EDGE, int kv) XT_INLINE {
     constexpr bool mn_edge = decltype(MN_EDGE)::value;
     constexpr bool k_edge = decltype(K_EDGE)::value;

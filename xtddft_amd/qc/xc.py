@@ -46,6 +46,33 @@ long-range K at XTDA.py:150-151, 527-539):
                     gives B88, omega -> inf gives zero), the series / closed-form match, and the
                     SCF's energy stationarity (tests/test_qc.py).
 
+PBE family (the reference's demo list, XTDA.py:1524-1531: 'pbe0', 'pbe38'):
+
+* PBE exchange      Perdew, Burke, Ernzerhof, PRL 77, 3865 (1996): per spin (spin scaling)
+                    e = -C_x (2 rho_s)^(4/3) F(s) / 2, F = 1 + kappa - kappa / (1 + mu s^2 / kappa),
+                    kappa = 0.804, mu = 0.2195149727645171, s = |grad n| / (2 (3 pi^2)^(1/3) n^(4/3))
+* PBE correlation   PW92 (PW_MOD) + H(rs, zeta, t) -- the same expression TPSS builds on
+PBE = PBE x + PBE c, PBE0 = 0.25 HF + 0.75 PBE x + PBE c, PBE38 = 0.375 HF + 0.625 PBE x +
+PBE c.  Pinned by the hydrogen atom (tests/test_qc.py): E_x^PBE = -0.3059 and E_c^PBE = -0.0060 Ha
+on the exact density (Perdew, Burke, Ernzerhof's table), E_x^LDA = -0.2680.
+
+omegaB97X-D (Chai and Head-Gordon, PCCP 10, 6615 (2008); the reference's 'wb97xd', XTDA.py:1528):
+B97-type power series in u = gamma s^2 / (1 + gamma s^2), s_s^2 = |grad rho_s|^2 / rho_s^(8/3):
+
+* exchange          sum_s e_x,s^LSDA att(a_s) g_x(u_s), a_s = omega / (2 (6 pi^2 rho_s)^(1/3)), gamma 0.004
+                    (short-range LSDA: the erf attenuation of the ITYH piece with the LDA Fermi wave vector)
+* correlation       same-spin PW92(rho_s, 0) g_ss(u_s) (gamma 0.2) + opposite-spin
+                    [n PW92(n, zeta) - sum_s PW92(rho_s, 0)] g_os(u_avg), s_avg^2 = (s_a^2 + s_b^2) / 2
+                    (gamma 0.006), the Stoll partition
+* coefficients      c_x = 0.777964, 0.661160, 0.574541, -5.25671, 11.6386;
+                    c_ss = 1, -6.90539, 31.3343, -51.0533, 26.4423;
+                    c_os = 1, 1.79413, -12.0477, 14.0847, -8.50809;
+                    HF exchange 0.222036 short-range + 1.0 long-range, omega = 0.2:
+                    PySCF's (omega, alpha, hyb) = (0.2, 1.0, 0.222036).
+The empirical -D dispersion energy depends on the nuclei only: it shifts E_tot and nothing else
+(no orbital, no response term) and is not added.  Parity unpinned (no reference printout);
+checked by its limits: the uniform-gas limit of the series (g(0) = c_0) and omega -> 0.
+
 TPSS = TPSS x + TPSS c, TPSSh = 0.1 HF + 0.9 TPSS x + TPSS c.  Pinned by two exact
 properties of the functional (tests/test_qc.py): the hydrogen-atom exchange energy is
 exactly -5/16 Ha and the correlation energy of any one-electron density is zero.
@@ -70,7 +97,7 @@ DENS_THRESHOLD = 1e-14
 _ZETA_MAX = 1.0 - 1e-10          # |zeta| cap (libxc's zeta threshold): (1 -+ zeta)^(-4/3) stays finite
 # spin-separable exchange pieces: each spin channel's half is screened on its own
 # density, as libxc does for exchange; correlation sees both channels unscreened
-_EXCHANGE = ("slater", "b88", "tpss_x")
+_EXCHANGE = ("slater", "b88", "tpss_x", "pbe_x")
 
 _CX = 1.5 * (3.0 / (4.0 * math.pi)) ** (1.0 / 3.0)
 
@@ -88,9 +115,13 @@ _FUNCTIONALS = {
     "TPSS": ([("tpss_x", 1.0), ("tpss_c", 1.0)], 0.0, "MGGA"),
     "TPSSH": ([("tpss_x", 0.9), ("tpss_c", 1.0)], 0.1, "MGGA"),
     "CAMB3LYP": ([("b88", 0.35), ("ityh_b88@0.33", 0.46), ("vwn5", 0.19), ("lyp", 0.81)], 0.19, "GGA"),
+    "PBE": ([("pbe_x", 1.0), ("pbe_c", 1.0)], 0.0, "GGA"),
+    "PBE0": ([("pbe_x", 0.75), ("pbe_c", 1.0)], 0.25, "GGA"),
+    "PBE38": ([("pbe_x", 0.625), ("pbe_c", 1.0)], 0.375, "GGA"),
+    "WB97XD": ([("wb97x_x@0.2", 1.0), ("wb97x_c", 1.0)], 0.222036, "GGA"),
 }
 # range-separated hybrids: name -> (omega, alpha) with PySCF's meaning (hyb from the table above)
-_RSH = {"CAMB3LYP": (0.33, 0.65)}
+_RSH = {"CAMB3LYP": (0.33, 0.65), "WB97XD": (0.2, 1.0)}
 NCOMP = {"HF": 1, "LDA": 1, "GGA": 4, "MGGA": 5}
 
 
@@ -328,13 +359,74 @@ def _ityh_b88(ra, rb, saa, sab, sbb, torch, omega):
     return out
 
 
-_PIECES = {"slater": _slater, "b88": _b88, "lyp": _lyp, "vwn5": _vwn5, "vwn_rpa": _vwn_rpa}
+def _pbe_x(ra, rb, saa, sab, sbb, torch):
+    """PBE exchange, spin-scaled: sum_s E_x^unpol[2 rho_s] / 2."""
+    kappa, mu = 0.804, 0.2195149727645171
+    out = 0.0
+    for r, sg in ((ra, saa), (rb, sbb)):
+        n, sig = 2.0 * r, 4.0 * sg
+        s2 = sig / (4.0 * (3.0 * math.pi ** 2) ** (2.0 / 3.0) * n ** (8.0 / 3.0))
+        fx = 1.0 + kappa - kappa / (1.0 + mu * s2 / kappa)
+        out = out - 0.5 * _CX * 2.0 ** (-1.0 / 3.0) * n ** (4.0 / 3.0) * fx
+    return out
+
+
+def _pbe_c(ra, rb, saa, sab, sbb, torch):
+    n = ra + rb
+    zeta = torch.clamp((ra - rb) / n, -_ZETA_MAX, _ZETA_MAX)
+    return n * _ec_pbe(n, zeta, saa + 2.0 * sab + sbb, torch)
+
+
+_WB97XD = dict(cx=(0.777964, 0.661160, 0.574541, -5.25671, 11.6386),
+               css=(1.0, -6.90539, 31.3343, -51.0533, 26.4423),
+               cos=(1.0, 1.79413, -12.0477, 14.0847, -8.50809))
+
+
+def _b97_g(c, gamma, s2):
+    u = gamma * s2 / (1.0 + gamma * s2)
+    out = 0.0
+    for ci in reversed(c):
+        out = out * u + ci
+    return out
+
+
+def _wb97x_x(ra, rb, saa, sab, sbb, torch, omega):
+    """omegaB97X short-range exchange: sum_s e_x,s^LSDA att(omega / 2 k_F,s) g_x(s_s^2)."""
+    out = 0.0
+    for r, sg in ((ra, saa), (rb, sbb)):
+        r13 = r ** (1.0 / 3.0)
+        r43 = r * r13
+        kf = (6.0 * math.pi ** 2) ** (1.0 / 3.0) * r13
+        out = out - _CX * r43 * _att_erf(omega / (2.0 * kf), torch) * _b97_g(_WB97XD["cx"], 0.004, sg / (r43 * r43))
+    return out
+
+
+def _wb97x_c(ra, rb, saa, sab, sbb, torch):
+    """omegaB97X correlation: same-spin and opposite-spin PW92 (Stoll partition) x B97 series."""
+    n = ra + rb
+    zeta = torch.clamp((ra - rb) / n, -_ZETA_MAX, _ZETA_MAX)
+    one = torch.full_like(n, _ZETA_MAX)
+    ess = 0.0
+    s2 = []
+    for r, sg in ((ra, saa), (rb, sbb)):
+        e_s = r * _ec_pw92(r, one, torch)
+        x2 = sg / r ** (8.0 / 3.0)
+        s2.append(x2)
+        ess = ess + e_s * _b97_g(_WB97XD["css"], 0.2, x2)
+    e_os = n * _ec_pw92(n, zeta, torch) - ra * _ec_pw92(ra, one, torch) - rb * _ec_pw92(rb, one, torch)
+    return ess + e_os * _b97_g(_WB97XD["cos"], 0.006, 0.5 * (s2[0] + s2[1]))
+
+
+_PIECES = {"slater": _slater, "b88": _b88, "lyp": _lyp, "vwn5": _vwn5, "vwn_rpa": _vwn_rpa,
+           "pbe_x": _pbe_x, "pbe_c": _pbe_c, "wb97x_c": _wb97x_c}
 _MPIECES = {"tpss_x": _tpss_x, "tpss_c": _tpss_c}
 
 
 def _piece(name, ra, rb, saa, sab, sbb, ta, tb, torch):
     if name.startswith("ityh_b88@"):
         return _ityh_b88(ra, rb, saa, sab, sbb, torch, float(name.split("@")[1]))
+    if name.startswith("wb97x_x@"):
+        return _wb97x_x(ra, rb, saa, sab, sbb, torch, float(name.split("@")[1]))
     if name in _MPIECES:
         return _MPIECES[name](ra, rb, saa, sab, sbb, ta, tb, torch)
     return _PIECES[name](ra, rb, saa, sab, sbb, torch)
@@ -347,7 +439,7 @@ def _energy_density(comps, ra, rb, saa, sab, sbb, ta, tb, torch, on=None):
     constants, so no derivative reaches the vanishing channel)."""
     eps = 0.0
     for name, coef in comps:
-        if on is not None and (name in _EXCHANGE or name.startswith("ityh_b88@")):
+        if on is not None and (name in _EXCHANGE or name.startswith(("ityh_b88@", "wb97x_x@"))):
             tiny = torch.full_like(ra, 1e-30).detach()
             zero = torch.zeros_like(ra).detach()
             half_a = _piece(name, ra, tiny, saa, zero, zero, ta, None if tb is None else tiny, torch)
