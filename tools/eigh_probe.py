@@ -1,6 +1,7 @@
 """Host eigh at Davidson subspace sizes on this box's CPU, one thread: SciPy (OpenBLAS)
 drivers evr (SciPy's default) / evd against torch's CPU eigh (MKL syevd) -- which host
-LAPACK the replicated Davidson step should call (xtddft_amd/davidson.py)."""
+LAPACK the replicated Davidson step should call (xtddft_amd/davidson.py); and the device
+eigh (torch.linalg.eigh on the GPU: rocSOLVER) for comparison."""
 import json
 import time
 
@@ -19,9 +20,15 @@ def main():
             a = rng.standard_normal((n, n))
             a = a + a.T
             row = {}
+            ad = torch.from_numpy(a).cuda() if torch.cuda.is_available() else None
+
+            def gpu():
+                w, v = torch.linalg.eigh(ad)
+                torch.cuda.synchronize()
             for name, f in (("scipy_evr", lambda: scipy.linalg.eigh(a)),
                             ("scipy_evd", lambda: scipy.linalg.eigh(a, driver="evd")),
-                            ("torch_mkl", lambda: torch.linalg.eigh(torch.from_numpy(a)))):
+                            ("torch_mkl", lambda: torch.linalg.eigh(torch.from_numpy(a)))) + \
+                    ((("gpu_syevd", gpu),) if ad is not None else ()):
                 f()
                 ts = []
                 for _ in range(5):

@@ -54,6 +54,13 @@ def cholesky_packed(mol, tol: float = 1e-12, device: int = 0, batch: int = 24, s
     tab = pair_table(mol)
     dv = torch.device(f"cuda:{device}")
     t0 = time.perf_counter()
+    split = dict(diag=0.0, columns=0.0, gemm=0.0, pivot=0.0)
+
+    def lap(name, t):
+        torch.cuda.synchronize(dv)
+        now = time.perf_counter()
+        split[name] += now - t
+        return now
     with torch.cuda.device(dv):
         D, q = eri_diag_device(mol, device, omega)
         D = D.clone()
@@ -64,6 +71,7 @@ def cholesky_packed(mol, tol: float = 1e-12, device: int = 0, batch: int = 24, s
         nvec = 0
         nbatch = ncols = 0
         pmax = torch.empty(tab.npair, dtype=torch.float64, device=dv)
+        t = lap("diag", t0)
         while True:
             dmax = float(D.max())
             if dmax <= tol:
@@ -74,11 +82,13 @@ def cholesky_packed(mol, tol: float = 1e-12, device: int = 0, batch: int = 24, s
             cand = torch.nonzero(pmax > cut).flatten()
             cand = cand[torch.argsort(pmax[cand], descending=True)][:batch].cpu().numpy()
             cols, M = eri_columns_device(mol, cand, q, SCREEN, device, omega)
+            t = lap("columns", t)
             nbatch += 1
             ncols += len(cols)
             tcols = torch.as_tensor(cols, device=dv)
             if nvec:
                 _gemm_tn_sub(L, V[:nvec], V[:nvec][:, tcols].contiguous(), M, device)
+            t = lap("gemm", t)
             while True:
                 dq = D[tcols]
                 iq = int(torch.argmax(dq))
@@ -97,10 +107,11 @@ def cholesky_packed(mol, tol: float = 1e-12, device: int = 0, batch: int = 24, s
                 D[tcols[iq]] = 0.0
                 M -= torch.outer(v, v[tcols])
             D.clamp_(min=0.0)
+            t = lap("pivot", t)
         torch.cuda.synchronize(dv)
     if stats is not None:
         stats.update(naux=nvec, batches=nbatch, columns=ncols, seconds=time.perf_counter() - t0,
-                     npack=npack, tol=tol)
+                     npack=npack, tol=tol, split_s={k: round(v, 3) for k, v in split.items()})
     return V[:nvec]
 
 

@@ -39,6 +39,7 @@ from .ints import AuxShellSet, ShellPair
 
 POINT_CHARGE_EXP = 1e24
 AO_MAX_L = 4
+PRIM_SCREEN = 1e-18       # primitive pairs below this bound are dropped (PairTable)
 
 
 def _torch():
@@ -57,23 +58,36 @@ class PairTable:
         pinfo, pprim, eab, pairs = [], [], [], []
         c0s, s0s = [], []
         crow = srow = q0 = e0 = 0
+        self.nprim_pairs = self.nprim_pairs_kept = 0
         for i in range(len(sh)):
             for j in range(i + 1):
                 sp = ShellPair(sh[i], sh[j])
-                nca, ncb, _, npp = sp.Eab.shape
+                # primitive-pair screening: a primitive pair whose Hermite coefficients are
+                # negligible (the Gaussian product factor exp(-ab/(a+b) |AB|^2) of two tight
+                # primitives on different atoms) contributes below PRIM_SCREEN to every
+                # integral -- its overlap-scale magnitude bounds its share of any (ab|cd),
+                # (ab|P) or <a|V|b> (the max(1, sqrt p) covers the 1/p of the Coulomb kernel
+                # against point charges); dropped from the kernels' loops
+                bound = (np.abs(sp.Eab).reshape(-1, sp.p.size).max(axis=0)
+                         * (np.pi / sp.p) ** 1.5 * np.maximum(1.0, np.sqrt(sp.p)))
+                keep = bound >= PRIM_SCREEN
+                self.nprim_pairs += sp.p.size
+                self.nprim_pairs_kept += int(keep.sum())
+                eab_k = np.ascontiguousarray(sp.Eab[..., keep])
+                nca, ncb, _, npp = eab_k.shape
                 pinfo.append([sh[i].l, sh[j].l, npp, q0, e0, crow, 0, 0])
-                pprim.append(np.column_stack([sp.p, sp.P]))
-                eab.append(sp.Eab.ravel())
+                pprim.append(np.column_stack([sp.p[keep], sp.P[keep]]))
+                eab.append(eab_k.ravel())
                 pairs.append((i, j))
                 c0s.append(crow)
                 s0s.append(srow)
                 crow += nca * ncb
                 srow += sh[i].nsph * sh[j].nsph
                 q0 += npp
-                e0 += sp.Eab.size
+                e0 += eab_k.size
         self.pinfo = np.array(pinfo, dtype=np.int32)
-        self.pprim = np.concatenate(pprim)
-        self.eab = np.concatenate(eab)
+        self.pprim = np.concatenate(pprim) if any(x.size for x in pprim) else np.zeros((1, 4))
+        self.eab = np.concatenate(eab) if any(x.size for x in eab) else np.zeros(1)
         self.pairs = pairs
         self.npair = len(pairs)
         self.c0 = np.array(c0s, dtype=np.int64)
