@@ -35,7 +35,7 @@ import numpy as np
 
 from .. import _capi
 from .gto import _sph_transform
-from .ints import AuxShellSet, ShellPair
+from .ints import AuxShellSet, ShellPair, ShellPairBatch, pair_classes
 
 POINT_CHARGE_EXP = 1e24
 AO_MAX_L = 4
@@ -59,24 +59,32 @@ class PairTable:
         c0s, s0s = [], []
         crow = srow = q0 = e0 = 0
         self.nprim_pairs = self.nprim_pairs_kept = 0
+        # Hermite tables of every pair, vectorised over the pairs of a class (ShellPairBatch)
+        tabs = [None] * (len(sh) * (len(sh) + 1) // 2)
+        for kk, ii, jj in pair_classes(sh):
+            bt = ShellPairBatch([sh[i] for i in ii], [sh[j] for j in jj])
+            # primitive-pair screening: a primitive pair whose Hermite coefficients are
+            # negligible (the Gaussian product factor exp(-ab/(a+b) |AB|^2) of two tight
+            # primitives on different atoms) contributes below PRIM_SCREEN to every
+            # integral -- its overlap-scale magnitude bounds its share of any (ab|cd),
+            # (ab|P) or <a|V|b> (the max(1, sqrt p) covers the 1/p of the Coulomb kernel
+            # against point charges); dropped from the kernels' loops
+            bound = (np.abs(bt.Eab).reshape(len(ii), -1, bt.p.shape[1]).max(axis=1)
+                     * (np.pi / bt.p) ** 1.5 * np.maximum(1.0, np.sqrt(bt.p)))
+            for m, k in enumerate(kk):
+                keep = bound[m] >= PRIM_SCREEN
+                tabs[k] = (np.ascontiguousarray(bt.Eab[m][..., keep]), bt.p[m][keep], bt.P[m][keep])
+                self.nprim_pairs += keep.size
+                self.nprim_pairs_kept += int(keep.sum())
+        k = 0
         for i in range(len(sh)):
             for j in range(i + 1):
-                sp = ShellPair(sh[i], sh[j])
-                # primitive-pair screening: a primitive pair whose Hermite coefficients are
-                # negligible (the Gaussian product factor exp(-ab/(a+b) |AB|^2) of two tight
-                # primitives on different atoms) contributes below PRIM_SCREEN to every
-                # integral -- its overlap-scale magnitude bounds its share of any (ab|cd),
-                # (ab|P) or <a|V|b> (the max(1, sqrt p) covers the 1/p of the Coulomb kernel
-                # against point charges); dropped from the kernels' loops
-                bound = (np.abs(sp.Eab).reshape(-1, sp.p.size).max(axis=0)
-                         * (np.pi / sp.p) ** 1.5 * np.maximum(1.0, np.sqrt(sp.p)))
-                keep = bound >= PRIM_SCREEN
-                self.nprim_pairs += sp.p.size
-                self.nprim_pairs_kept += int(keep.sum())
-                eab_k = np.ascontiguousarray(sp.Eab[..., keep])
+                eab_k, p_k, P_k = tabs[k]
+                tabs[k] = None
+                k += 1
                 nca, ncb, _, npp = eab_k.shape
                 pinfo.append([sh[i].l, sh[j].l, npp, q0, e0, crow, 0, 0])
-                pprim.append(np.column_stack([sp.p[keep], sp.P[keep]]))
+                pprim.append(np.column_stack([p_k, P_k]))
                 eab.append(eab_k.ravel())
                 pairs.append((i, j))
                 c0s.append(crow)

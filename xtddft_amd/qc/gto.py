@@ -213,23 +213,26 @@ class Mole:
 
     # ----------------------------------------------------------- integrals
     def _ovlp_kin(self):
-        """int1e_ovlp and int1e_kin in one pass over the shell pairs (the pair's
-        Hermite tables, extended for the kinetic operator, serve both); cached."""
+        """int1e_ovlp and int1e_kin in one pass over the shell pairs, vectorised over the
+        pairs of each class (``ints.ShellPairBatch``; the pair's Hermite tables, extended
+        for the kinetic operator, serve both); cached."""
         if "kin" not in self._int1e:
+            from .ints import ShellPairBatch, pair_classes
             n = self._nao
             S, T = np.zeros((n, n)), np.zeros((n, n))
             sh = self.shells
-            for i, si in enumerate(sh):
-                Ti = _sph_transform(si.l)
-                a0, a1 = self.ao_loc[i], self.ao_loc[i + 1]
-                for j in range(i + 1):
-                    Tj = _sph_transform(sh[j].l)
-                    b0, b1 = self.ao_loc[j], self.ao_loc[j + 1]
-                    pair = ShellPair(si, sh[j], kin=True, hermite=False)
-                    for out, blk in ((S, pair.overlap()), (T, pair.kinetic())):
-                        blk = Ti @ blk @ Tj.T
-                        out[a0:a1, b0:b1] = blk
-                        out[b0:b1, a0:a1] = blk.T
+            loc = self.ao_loc
+            for _, ii, jj in pair_classes(sh):
+                batch = ShellPairBatch([sh[i] for i in ii], [sh[j] for j in jj], kin=True, hermite=False)
+                Ti, Tj = _sph_transform(sh[ii[0]].l), _sph_transform(sh[jj[0]].l)
+                mi, nj = Ti.shape[0], Tj.shape[0]
+                rows = loc[ii][:, None, None] + np.arange(mi)[None, :, None]
+                cols = loc[jj][:, None, None] + np.arange(nj)[None, None, :]
+                rows, cols = np.broadcast_arrays(rows, cols)
+                for out, blk in ((S, batch.overlap()), (T, batch.kinetic())):
+                    blk = np.einsum('mi,pij,nj->pmn', Ti, blk, Tj)
+                    out[rows, cols] = blk
+                    out[cols, rows] = blk
             nrm = self._norm[:, None] * self._norm[None, :]
             self._int1e["ovlp"], self._int1e["kin"] = S * nrm, T * nrm
         return self._int1e["ovlp"].copy(), self._int1e["kin"].copy()
