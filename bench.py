@@ -55,7 +55,8 @@ HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8.0 TB/s spec
 ROUND = 6
 PMC_SUMMARY = os.path.join(ROOT, "profiles", f"r{ROUND:02d}_pmc_summary.json")
 
-CPU_CONVERGE_AUTO_S = 60.0   # bench's default run times the CPU Davidson only when it is this short
+CPU_CONVERGE_AUTO_S = 60.0
+WARM_FULL_DIM = 20000        # converge(): a whole untimed warm-up solve below this dimension   # bench's default run times the CPU Davidson only when it is this short
 
 KIND_NAME = {"XTDA": "X-TDA", "SF_UP": "SF-TDA (spin-flip up)", "SF_DOWN": "SF-TDA (spin-flip down)",
              "XSF": "XSF-TDA"}
@@ -439,9 +440,9 @@ def _solver_setup(args, w, dev):
 
 def converge(args, w, allreduce, world=1):
     """Wall time of the device Davidson to nroots under the reference's criteria (operator
-    construction included).  An untimed 2-iteration solve first loads the solver's kernels
-    (first-launch costs are not per-solve work); the replicated solver of a sharded
-    operator runs with the lockstep guard."""
+    construction included).  An untimed solve first loads the solver's kernels (first-launch
+    costs are not per-solve work: the whole solve up to WARM_FULL_DIM, 2 iterations above);
+    the replicated solver of a sharded operator runs with the lockstep guard."""
     import torch
     from xtddft_amd.davidson import davidson1
     op, dev = w.op, w.device
@@ -461,7 +462,9 @@ def converge(args, w, allreduce, world=1):
         stats["s"] += t1 - t
         stats["allreduce_s"] += time.perf_counter() - t1
         return s
-    warm = dict(kw, max_cycle=2)
+    # small operators: the whole solve (seconds at most), so every solver path -- dropped
+    # vectors, restarts -- has loaded its kernels; large ones: two iterations
+    warm = dict(kw, max_cycle=2) if op.dim > WARM_FULL_DIM else kw
     davidson1(lambda xt: allreduce(op.apply(xt)), x0, pre, nroots=args.nroots, device=dev.index,
               return_device=True, lockstep=world > 1, **warm)
     torch.cuda.synchronize()
@@ -484,7 +487,8 @@ def converge(args, w, allreduce, world=1):
                 solver_phase_ms={k: round(1e3 * v, 2) for k, v in phase_s.items()},
                 nvec_histogram={str(k): v for k, v in sorted(hist.items())},
                 e_min_ha=float(e[0]), e_ha=[float(v) for v in e], criteria=crit,
-                warmup="an untimed 2-iteration solve first (solver kernels loaded)")
+                warmup=("an untimed " + ("2-iteration solve" if op.dim > WARM_FULL_DIM else "solve")
+                        + " first (solver kernels loaded)"))
 
 
 def cpu_converge(args, w, gpu):
