@@ -161,6 +161,9 @@ def main():
     ap.add_argument("--explicit-max", type=int, default=12000,
                     help="largest dim checked through the oracle's explicit A; above it, sigma parity")
     ap.add_argument("--scf-only", action="store_true")
+    ap.add_argument("--factor-host", default="auto", choices=("auto", "on", "off"),
+                    help="after the SCF, keep the AO Cholesky factor in host memory instead of HBM "
+                         "(auto: nao >= 600), so the operator's stored exchange fits beside its MO factor")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     spec = MOLECULES[a.molecule]
@@ -215,6 +218,15 @@ def main():
     mfield = mf.to_meanfield()
     torch.cuda.synchronize()
     rec["meanfield_s"] = round(time.perf_counter() - t0, 3)
+    if a.factor_host == "on" or (a.factor_host == "auto" and mol.nao >= 600):
+        # the operator transforms the AO factor to its MO factor once (xt_set_jk_df stages host
+        # input in chunks); the SCF's HBM copy (54 GB for C60 at tol 1e-8) would otherwise keep
+        # the stored MO exchange out of HBM (the auto rule takes the free memory)
+        mfield.cderi = mfield.cderi.cpu() if hasattr(mfield.cderi, "cpu") else mfield.cderi
+        mf.cderi_exact = None
+        mf.device_engine = None
+        torch.cuda.empty_cache()
+        rec["factor_in_host_memory"] = True
     phase["name"] = f"{a.kind} solve"
     if a.kind == "sfup":
         from xtddft_amd.sf_tda import DAVIDSON_SAMPLES, SF_TDA
@@ -225,7 +237,7 @@ def main():
         e = np.asarray(td.e)[:nstates]
         op = td._op
         rec.update(xtda_s=round(time.perf_counter() - t0, 3), xtda_converged=bool(np.all(td.converged)),
-                   method=a.method, dim=int(op.dim), roots_ha=[float(x) for x in e])
+                   method=a.method, dim=int(op.dim), k_mode=op.k_mode, roots_ha=[float(x) for x in e])
         x = np.ascontiguousarray(np.asarray(td.v)[:, :nstates].T)
         rec["max_residual"] = float(np.linalg.norm(op.apply_full(x) - e[:, None] * x, axis=1).max())
         print("sfup", rec["xtda_s"], e[:5], flush=True)
