@@ -129,6 +129,21 @@ def test_xc_kernels_small_batches(hiplib, env, knobs, nz, nc, no, nao):
     assert rel(op.apply(z), vind(z)) < RTOL
 
 
+@pytest.mark.parametrize("nz", [3, 5, 8, 11])
+def test_xc_small_o_tail_split(hiplib, env, nz):
+    """The small-O rho-forward on a grid of more 64-point blocks than the chip has CUs
+    (20 000 points: 313 blocks = 256 + 57 on 256 CUs): the last round's blocks split their
+    trial pairs 4 ways (nx = 16, 22), 2 ways (nx = 10) or not at all (nx = 6) -- against the
+    oracle."""
+    from xtddft_amd.operator import DeviceOperator
+    env(XT_W_KERNEL=3)
+    mf = make_mf(nao=60, nc=33, no=1, ngrid=20000, xctype="GGA", hyb=0.2)
+    vind, hdiag = oxtda.gen_tda_operation(mf)
+    z = make_trial_vectors(nz, hdiag.size)
+    op = DeviceOperator(mf, "XTDA")
+    assert rel(op.apply(z), vind(z)) < RTOL
+
+
 @pytest.mark.parametrize("nz", [1, 3, 30])
 def test_sf_up_single_channel_small_batches(hiplib, nz):
     """SF-up (one channel: nx = nz, odd counts) through the same small-batch shapes."""

@@ -18,6 +18,10 @@
 //   * the rows4 reduction of a pair's per-lane partials runs once per (pair, chunk); the
 //     chunks of one pair are summed in the output (the same lane reads back what it wrote
 //     a chunk earlier; the old value is prefetched when the pair starts).
+//   * the blocks of the last, partial round over the CUs split their trial pairs S ways
+//     (pair subsets p = s (mod S)): that round then takes a fraction of a block time
+//     instead of a whole one (n = 200 000, 3125 = 12 x 256 + 53 blocks: 0.851 -> 0.821 ms
+//     at S = 4, tools/xcws_probe.hip).
 // Operand conventions are those of xc_rho_w (xt_internal.h): Zp readable 7 rows past O
 // and 31 columns past V (zeroed slack), PhiO / dPhiV rows past n are not read.
 #include <hip/hip_runtime.h>
@@ -58,7 +62,7 @@ k_xc_rho_ws(int O, int nx, int V, int n,
             const double* __restrict__ PO, long ldp,
             const double* __restrict__ Z, long zi, long zx,
             const double* __restrict__ Wg, long wc, long wg,
-            double* __restrict__ Rout, long rg) {
+            double* __restrict__ Rout, long rg, int nb_main, int split) {
   constexpr int NT = 64 * SW_NW, KP = KS / 2, KI = 4 * KS, ZD = KS;
   constexpr bool ODD = (KS & 1) != 0;
   constexpr int W_LD = 3 * SW_GB * SW_AC / NT;       // weight elements staged per thread and chunk (24)
@@ -71,10 +75,17 @@ k_xc_rho_ws(int O, int nx, int V, int n,
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4, r16 = lane & 15;
-  const int g0 = blockIdx.x * SW_GB;
+  // block -> 64-point block pb and pair subset {pbase + pstride j}: blocks past nb_main are
+  // the last round's point blocks, each split over `split` blocks
+  const int tb = (int)blockIdx.x - nb_main;
+  const int pb = tb < 0 ? (int)blockIdx.x : nb_main + tb / split;
+  const int pbase = tb < 0 ? 0 : tb % split, pstride = tb < 0 ? 1 : split;
+  const int g0 = pb * SW_GB;
   const int nat = (V + SW_WA - 1) / SW_WA;           // a-tiles
   const int nck = (nat + 1) / 2;                     // chunks of two a-tiles
-  const int npw = wave < nx ? (nx - wave + SW_NW - 1) / SW_NW : 0;   // pairs of this wave
+  const int nxs = (nx - pbase + pstride - 1) / pstride;   // pairs of the block
+  const int npw = wave < nxs ? (nxs - wave + SW_NW - 1) / SW_NW : 0;   // pairs of this wave
+  auto pair_of = [&](int pi) XT_INLINE { return pbase + pstride * (wave + SW_NW * pi); };
 
   // ---- PhiO tile -> LDS, once (rows past O and points past n as zero) ---------------
   for (int p = tid; p < KI * SW_GB; p += NT) {
@@ -93,7 +104,7 @@ k_xc_rho_ws(int O, int nx, int V, int n,
   const unsigned z_off1 = (unsigned)(((long)q * zi + r16) * 8);
   int wc_ = 0, wp_ = 0, wt_ = 0;                     // walker: chunk, pair index, tile in chunk
   auto unit_off = [&](int ch, int pi, int tc) XT_INLINE {
-    return (int)((((long)(wave + SW_NW * pi)) * zx + (long)(2 * ch + tc) * SW_WA) * 8);
+    return (int)((((long)pair_of(pi)) * zx + (long)(2 * ch + tc) * SW_WA) * 8);
   };
   auto advance = [&]() XT_INLINE {                   // walker -> next unit (stays on the last)
     const int ntc = 2 * wc_ + 1 < nat ? 2 : 1;
@@ -219,7 +230,7 @@ k_xc_rho_ws(int O, int nx, int V, int n,
     if (ch == 0) bfirst();
     const int ntc = 2 * ch + 1 < nat ? 2 : 1;
     for (int pi = 0; pi < npw; ++pi) {
-      const int xg = wave + SW_NW * pi;
+      const int xg = pair_of(pi);
       // the chunks before this one left partial sums in the output: prefetch them, lane
       // row q holding (and later storing) column sub-tile j = q
       const int go = g0 + 16 * q + r16;
@@ -257,11 +268,27 @@ int xc_rho_ws(int O, int nx, int V, int n, const double* PO, long ldp, const dou
   if (KS > SW_KS_MAX) return XT_ERR_ARG;
   // 32-bit buffer offsets over Zp: KI rows (+ the a-tile overhang) of zi doubles
   if ((double)(4 * KS + 1) * (double)zi * 8.0 >= 2147483647.0) return XT_ERR_ARG;
-  const int blocks = (n + SW_GB - 1) / SW_GB;
   static std::mutex mu;
   static unsigned long long done[SW_KS_MAX + 1] = {};
+  static int ncu[64] = {};
   int dev = 0;
   (void)hipGetDevice(&dev);
+  int cus = 256;
+  if (dev < 64) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!ncu[dev] && hipDeviceGetAttribute(&ncu[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu[dev] = 256;
+    cus = ncu[dev] > 0 ? ncu[dev] : 256;
+  }
+  // one block per CU (LDS): the last round's point blocks split their pairs S ways when
+  // each part keeps >= 4 pairs and the parts still fit in one round
+  const int pblocks = (n + SW_GB - 1) / SW_GB;
+  const int tail = pblocks > cus ? pblocks % cus : 0;
+  int split = 1;
+  for (int sp = 4; sp >= 2 && split == 1; sp /= 2)
+    if (tail > 0 && tail * sp <= cus && nx >= 4 * sp) split = sp;
+  const int nb_main = pblocks - (split > 1 ? tail : 0);
+  const int blocks = nb_main + (split > 1 ? tail * split : 0);
 #define XT_WS(K)                                                                                           \
   case K: {                                                                                                \
     {                                                                                                      \
@@ -273,7 +300,7 @@ int xc_rho_ws(int O, int nx, int V, int n, const double* PO, long ldp, const dou
       }                                                                                                    \
     }                                                                                                      \
     hipLaunchKernelGGL((k_xc_rho_ws<K>), dim3(blocks), dim3(64 * SW_NW), SW_LDS, st, O, nx, V, n, PO, ldp, Z, \
-                       zi, zx, W, wc, wg, R, rg);                                                          \
+                       zi, zx, W, wc, wg, R, rg, nb_main, split);                                          \
     break;                                                                                                 \
   }
   switch (KS) {
