@@ -4,6 +4,7 @@
 //   DIAG bit 1: weights staged for chunk 0 only (no barrier / staging after it)
 //   DIAG bit 2: Zp loaded once (the ring is never refilled)
 //   DIAG bit 3: no per-pair output (rows4 reduction, partial-sum load, store)
+//   DIAG bit 6: chunks past 0 keep their barriers but stage no global loads (LDS writes of a constant)
 //   DIAG bits 4-5: waves 4..7 sleep 16 / 32 / 64 x 64 cycles after each chunk barrier (phase stagger)
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I xtddft_amd/csrc tools/xcws_probe.hip -o tools/bin/xcws_probe
 // Run:   tools/bin/xcws_probe O nx V n [reps]
@@ -161,7 +162,8 @@ k_probe(int O, int nx, int V, int n, const double* __restrict__ PO, long ldp, co
 #pragma unroll
     for (int k = 0; k < W_LD; ++k) {
       const int g = g0 + wr + 8 * (k % 8);
-      rw[k] = (a < V && g < n) ? Wg[(long)(k / 8) * wc + (long)g * wg + a] : 0.0;
+      if ((DIAG & 64) && ch > 0) rw[k] = 0.5;
+      else rw[k] = (a < V && g < n) ? Wg[(long)(k / 8) * wc + (long)g * wg + a] : 0.0;
     }
 #pragma unroll
     for (int k = 0; k < W_LD; ++k) sW[((k / 8) * SW_GB + wr + 8 * (k % 8)) * SW_WP + wa] = rw[k];
@@ -288,6 +290,7 @@ int main(int argc, char** argv) {
     rep("Zp once (4)", run_probe<4>(O, nx, V, n, P, ldp, Z, zi, zx, W + 34, wc, wg, R1, rg, reps));
     rep("MFMA only (7)", run_probe<7>(O, nx, V, n, P, ldp, Z, zi, zx, W + 34, wc, wg, R1, rg, reps));
     rep("MFMA only, no output (15)", run_probe<15>(O, nx, V, n, P, ldp, Z, zi, zx, W + 34, wc, wg, R1, rg, reps));
+    rep("barriers, no staging loads (64)", run_probe<64>(O, nx, V, n, P, ldp, Z, zi, zx, W + 34, wc, wg, R1, rg, reps));
     rep("stagger 16 (16)", run_probe<16>(O, nx, V, n, P, ldp, Z, zi, zx, W + 34, wc, wg, R1, rg, reps));
     rep("stagger 32 (32)", run_probe<32>(O, nx, V, n, P, ldp, Z, zi, zx, W + 34, wc, wg, R1, rg, reps));
     rep("stagger 64 (48)", run_probe<48>(O, nx, V, n, P, ldp, Z, zi, zx, W + 34, wc, wg, R1, rg, reps));
