@@ -15,8 +15,13 @@ Cholesky vectors -- computed here without the 4-index array ever existing
   first), evaluate their columns (all pairs | those pairs) with the integral kernel
   (Schwarz-screened), subtract the existing vectors' contribution with one GEMM
   (``xt_dgemm``), then pivot inside the batch -- new vectors are taken while the
-  batch's residual diagonal exceeds max(tol, spread x D_max) -- each a rank-one
-  update of the batch columns and the diagonal.
+  batch's residual diagonal exceeds max(tol, spread x D_max).  The pivoting runs on
+  the batch's own (ncols x ncols) residual block on the host (``_batch_pivots``: the
+  pivot order and the new vectors' values at the batch pairs), then every new vector
+  at once on the device by one triangular solve, V_new^T = Lp^-1 M[:, piv]^T, and the
+  diagonal by one sum of squares -- the same vectors as a rank-one update of the
+  (npack x ncols) columns per pivot (C60 / cc-pVDZ: 11 954 of them, 9.5 s), in a few
+  device calls per batch.
 
 The result is exact to ``tol``: every residual diagonal is <= tol at exit, so by
 Cauchy-Schwarz every |(mu nu|la si) - sum_P L L| <= tol.  Vectors live in the
@@ -28,10 +33,13 @@ from __future__ import annotations
 import ctypes
 import math
 
+import numpy as np
+
 from .. import _capi
 from .dints import eri_columns_device, eri_diag_device, pair_table
 
 SCREEN = 1e-15        # Schwarz threshold (absolute), far below any factorisation tol
+TRSM_COLS = 8192      # packed columns per triangular solve
 
 
 def _gemm_tn_sub(L, a, b, c, device):
@@ -42,6 +50,28 @@ def _gemm_tn_sub(L, a, b, c, device):
     n = b.shape[1]
     _capi.check(L.xt_dgemm(1, 0, m, n, k, -1.0, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), 1.0,
                            c.data_ptr(), c.stride(0), ctypes.c_void_p(st)), "xt_dgemm")
+
+
+def _batch_pivots(C: np.ndarray, d: np.ndarray, cut: float):
+    """Pivoted Cholesky of one batch's residual block C (ncols x ncols, symmetric) with
+    residual diagonal d: pivots are taken largest-first while d > cut.  Returns the
+    pivot columns and Lb (ncols x r), the new vectors' values at the batch pairs
+    (column k = vector k)."""
+    n = d.size
+    d = d.astype(np.float64, copy=True)
+    Lb = np.zeros((n, n))
+    piv = []
+    for k in range(n):
+        iq = int(np.argmax(d))
+        dk = d[iq]
+        if dk <= cut:
+            break
+        col = (C[:, iq] - Lb[:, :k] @ Lb[iq, :k]) / math.sqrt(dk)
+        Lb[:, k] = col
+        d -= col * col
+        d[iq] = 0.0
+        piv.append(iq)
+    return np.asarray(piv, dtype=np.int64), Lb[:, :len(piv)]
 
 
 def cholesky_packed(mol, tol: float = 1e-12, device: int = 0, batch: int = 24, spread: float = 0.01,
@@ -89,24 +119,30 @@ def cholesky_packed(mol, tol: float = 1e-12, device: int = 0, batch: int = 24, s
             if nvec:
                 _gemm_tn_sub(L, V[:nvec], V[:nvec][:, tcols].contiguous(), M, device)
             t = lap("gemm", t)
-            while True:
-                dq = D[tcols]
-                iq = int(torch.argmax(dq))
-                d = float(dq[iq])
-                if d <= cut:
-                    break
-                if nvec == V.shape[0]:
+            piv, Lb = _batch_pivots(M[tcols].cpu().numpy(), D[tcols].cpu().numpy(), cut)
+            r = piv.size
+            if r:
+                while nvec + r > V.shape[0]:
                     grow = min(npack, 2 * V.shape[0]) - V.shape[0]
                     if grow <= 0:
                         raise RuntimeError("Cholesky rank exceeds the number of pairs")
                     V = torch.cat([V, torch.empty((grow, npack), dtype=torch.float64, device=dv)])
-                v = M[:, iq] / math.sqrt(d)
-                V[nvec] = v
-                nvec += 1
-                D -= v * v
-                D[tcols[iq]] = 0.0
-                M -= torch.outer(v, v[tcols])
+                # vector k = (M[:, piv_k] - sum_{j<k} v_j Lb[piv_k, j]) / Lb[piv_k, k]:
+                # Lp V_new^T = M[:, piv]^T with Lp = Lb[piv] lower triangular
+                tp = torch.as_tensor(piv, device=dv)
+                Lp = torch.as_tensor(Lb[piv], device=dv)
+                # (column blocks: one rocBLAS trsm over all npack columns asks for more
+                # workspace than torch hands hipBLAS and fails with ALLOC_FAILED)
+                vn = V[nvec:nvec + r]
+                for c0 in range(0, npack, TRSM_COLS):
+                    c1 = min(c0 + TRSM_COLS, npack)
+                    vn[:, c0:c1] = torch.linalg.solve_triangular(Lp, M[c0:c1, tp].T.contiguous(), upper=False)
+                nvec += r
+                D -= (vn * vn).sum(0)
+                D[tcols[tp]] = 0.0
             D.clamp_(min=0.0)
+            if r == 0 and float(D[tcols].max()) > cut:
+                raise RuntimeError("pivoted Cholesky made no progress on a batch")
             t = lap("pivot", t)
         torch.cuda.synchronize(dv)
     if stats is not None:
