@@ -30,6 +30,7 @@
 // _attenuate).
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <mutex>
 #include "xt_internal.h"
 
 namespace xt {
@@ -38,15 +39,17 @@ __host__ __device__ constexpr int ntuv(int L) { return (L + 1) * (L + 2) * (L + 
 __host__ __device__ constexpr int ncart(int l) { return (l + 1) * (l + 2) / 2; }
 // position of (t, u, v) in the order of qc/ints.py hermite_index: by n = t + u + v,
 // then t descending, then u descending
-__device__ inline int tuv_pos(int t, int u, int v) {
+__host__ __device__ constexpr int tuv_pos(int t, int u, int v) {
   const int n = t + u + v, d = n - t;
   return n * (n + 1) * (n + 2) / 6 + d * (d + 1) / 2 + (d - u);
 }
 
 // F_n(T), n = 0..m: the series for F_m and downward recursion below T = 30 (all
 // terms positive, no cancellation), F_0 = sqrt(pi/T) erf(sqrt T) / 2 and upward
-// recursion above (the amplification (2n+1)/(2T) < 1 for n <= 13 < T: stable)
-__device__ void boys_all(int m, double T, double* F) {
+// recursion above (the amplification (2n+1)/(2T) < 1 for n <= 13 < T: stable).
+// The series runs only to fill the table below (its ~T + 30 divisions per call made
+// the Boys function the bulk of an s-shell quartet's cost).
+__device__ void boys_series(int m, double T, double* F) {
   if (T < 30.0) {
     double term = 1.0 / (2 * m + 1), sum = term;
     for (int k = 1; k < 400; ++k) {
@@ -61,6 +64,40 @@ __device__ void boys_all(int m, double T, double* F) {
     const double et = exp(-T);
     F[0] = 0.5 * sqrt(M_PI / T) * erf(sqrt(T));
     for (int n = 0; n < m; ++n) F[n + 1] = ((2 * n + 1) * F[n] - et) / (2.0 * T);
+  }
+}
+
+// Tabulated F_n(T_i), T_i = i h on [0, 30], n <= BOYS_NM - 1: below T = 30, F_m(T) is the
+// 7-term Taylor series about the nearest T_i (dF_n/dT = -F_{n+1}; |T - T_i| <= h / 2 =
+// 0.025: remainder <= F_m 0.025^7 / 7! ~ 1.2e-15 relative), the lower orders by the
+// downward recursion from it.  Filled once per device by k_boys_init (the series above).
+constexpr int BOYS_NM = kIntMaxL + 7;
+constexpr int BOYS_NT = 601;
+constexpr double BOYS_H = 0.05;
+__device__ double g_boys_tab[BOYS_NT * BOYS_NM];
+
+__global__ void k_boys_init() {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < BOYS_NT) {
+    double F[BOYS_NM];
+    boys_series(BOYS_NM - 1, i * BOYS_H, F);
+    for (int n = 0; n < BOYS_NM; ++n) g_boys_tab[i * BOYS_NM + n] = F[n];
+  }
+}
+
+__device__ __forceinline__ void boys_all(int m, double T, double* F) {
+  if (T < 30.0) {
+    const int i = (int)(T * (1.0 / BOYS_H) + 0.5);
+    const double md = i * BOYS_H - T;            // -(T - T_i)
+    const double* f = g_boys_tab + i * BOYS_NM + m;
+    double v = f[6];
+#pragma unroll
+    for (int k = 5; k >= 0; --k) v = f[k] + md * (1.0 / (k + 1)) * v;
+    F[m] = v;
+    const double et = exp(-T);
+    for (int n = m - 1; n >= 0; --n) F[n] = (2.0 * T * F[n + 1] + et) * (1.0 / (2 * n + 1));
+  } else {
+    boys_series(m, T, F);
   }
 }
 
@@ -101,6 +138,103 @@ __device__ void hermite_r(int L, double alpha, double X, double Y, double Z, dou
   }
 }
 
+
+// ---- quartets of total Hermite order L = LAB + LC <= 6 (the contracted s / p shells: many
+// primitive quartets each) with compile-time (t, u, v) loops: the R table, the ket
+// contraction M and the bra contraction stay in registers (the runtime-L path below keeps
+// them in private memory and spends more scalar loop control than arithmetic).
+template <int L>
+__device__ __forceinline__ void hermite_rc(double alpha, double X, double Y, double Z, double (&R)[ntuv(L)]) {
+  double F[L + 1];
+  boys_all(L, alpha * (X * X + Y * Y + Z * Z), F);
+  const double m2a = -2.0 * alpha;
+  double pw[L + 1];
+  pw[0] = 1.0;
+#pragma unroll
+  for (int n = 0; n < L; ++n) pw[n + 1] = pw[n] * m2a;
+  // in place, one level at a time: level n at (t, u, v) reads level n + 1 at orders
+  // tot - 1 and tot - 2 only, so walking tot downwards overwrites nothing still needed
+  R[0] = pw[L] * F[L];
+#pragma unroll
+  for (int n = L - 1; n >= 0; --n) {
+#pragma unroll
+    for (int tot = L - n; tot >= 1; --tot)
+#pragma unroll
+      for (int t = tot; t >= 0; --t)
+#pragma unroll
+        for (int u = tot - t; u >= 0; --u) {
+          const int v = tot - t - u;
+          double val;
+          if (t > 0) {
+            val = X * R[tuv_pos(t - 1, u, v)];
+            if (t > 1) val += (t - 1) * R[tuv_pos(t - 2, u, v)];
+          } else if (u > 0) {
+            val = Y * R[tuv_pos(0, u - 1, v)];
+            if (u > 1) val += (u - 1) * R[tuv_pos(0, u - 2, v)];
+          } else {
+            val = Z * R[tuv_pos(0, 0, v - 1)];
+            if (v > 1) val += (v - 1) * R[tuv_pos(0, 0, v - 2)];
+          }
+          R[tuv_pos(t, u, v)] = val;
+        }
+    R[0] = pw[n] * F[n];
+  }
+}
+
+template <int LAB, int LC>
+__device__ __forceinline__ void quartet_cls(int npp, const double* __restrict__ pp0, const double* __restrict__ ea0,
+                                            int nab, int nr, const double* __restrict__ cp0,
+                                            const double* __restrict__ e0, int nc, double omega,
+                                            double* __restrict__ out, long ldo) {
+  constexpr int L = LAB + LC, NT = ntuv(LAB), NU = ntuv(LC);
+  for (int q = 0; q < npp; ++q) {
+    const double* pp = pp0 + 4 * (long)q;
+    const double p = pp[0];
+    for (int r = 0; r < nr; ++r) {
+      const double* cp = cp0 + 4 * (long)r;
+      const double s = cp[0];
+      double alpha = p * s / (p + s), scale = 1.0;
+      if (omega > 0.0) {
+        const double w2 = omega * omega, a2 = alpha * w2 / (alpha + w2);
+        scale = sqrt(a2 / alpha);
+        alpha = a2;
+      }
+      double R[ntuv(L)];
+      hermite_rc<L>(alpha, pp[1] - cp[1], pp[2] - cp[2], pp[3] - cp[3], R);
+      const double pref = 2.0 * pow(M_PI, 2.5) / (p * s * sqrt(p + s)) * scale;
+      for (int c = 0; c < nc; ++c) {
+        const double* e = e0 + ((long)c * NU) * nr + r;
+        double M[NT];
+#pragma unroll
+        for (int it = 0; it < NT; ++it) M[it] = 0.0;
+#pragma unroll
+        for (int nu = 0; nu <= LC; ++nu)
+#pragma unroll
+          for (int tu = nu; tu >= 0; --tu)
+#pragma unroll
+            for (int uu = nu - tu; uu >= 0; --uu) {
+              const int vu = nu - tu - uu, iu = tuv_pos(tu, uu, vu);
+              const double w = ((nu & 1) ? -1.0 : 1.0) * e[(long)iu * nr];
+#pragma unroll
+              for (int nt = 0; nt <= LAB; ++nt)
+#pragma unroll
+                for (int tt = nt; tt >= 0; --tt)
+#pragma unroll
+                  for (int ut = nt - tt; ut >= 0; --ut)
+                    M[tuv_pos(tt, ut, nt - tt - ut)] += w * R[tuv_pos(tt + tu, ut + uu, nt - tt - ut + vu)];
+            }
+        for (int ab = 0; ab < nab; ++ab) {
+          const double* ea = ea0 + ((long)ab * NT) * npp + q;
+          double acc = 0.0;
+#pragma unroll
+          for (int it = 0; it < NT; ++it) acc += ea[(long)it * npp] * M[it];
+          out[(long)ab * ldo + c] += pref * acc;
+        }
+      }
+    }
+  }
+}
+
 // pair_info[8 k + .]: la, lb, npp, prim0, e0, row0;  pair_prim[4 q + .]: p, Px, Py, Pz
 // ket_info[8 j + .]:  lc, nprim, prim0, e0, col0, nc; ket_prim[4 r + .]:  s, Cx, Cy, Cz
 // eab (pair k): [a][b][t][q] over ncart(la) x ncart(lb) x ntuv(la+lb) x npp
@@ -120,10 +254,10 @@ k_int_cart(int npair, const int* __restrict__ pair_info, const double* __restric
   if (diag) {
     if (id >= npair) return;
     k = j = (int)id;
-  } else {
+  } else {   // bra fastest: the table orders pairs by class (qc/dints.py PairTable)
     if (id >= (long)npair * nket) return;
-    k = (int)(id / nket);
-    j = (int)(id % nket);
+    j = (int)(id / npair);
+    k = (int)(id % npair);
   }
   if (q_bra != nullptr && q_bra[k] * q_ket[j] < q_thr) return;
   const int* pi = pair_info + 8 * k;
@@ -132,6 +266,22 @@ k_int_cart(int npair, const int* __restrict__ pair_info, const double* __restric
   const int lc = ai[0], nr = ai[1], ar0 = ai[2], ae0 = ai[3], col0 = ai[4];
   const int lab = la + lb, L = lab + lc;
   const int nab = ncart(la) * ncart(lb), ntab = ntuv(lab), nc = ai[5], ntc = ntuv(lc);
+  if (L <= 6 && lab <= 4 && lc <= 4) {
+    const double* pp0 = pair_prim + 4 * (long)pq0;
+    const double* cp0 = ket_prim + 4 * (long)ar0;
+    double* o = out + (long)row0 * ldo + col0;
+#define XT_QC(A, C) \
+  case 5 * A + C: quartet_cls<A, C>(npp, pp0, eab + pe0, nab, nr, cp0, ek + ae0, nc, omega, o, ldo); return;
+    switch (5 * lab + lc) {
+      XT_QC(0, 0) XT_QC(0, 1) XT_QC(0, 2) XT_QC(0, 3) XT_QC(0, 4)
+      XT_QC(1, 0) XT_QC(1, 1) XT_QC(1, 2) XT_QC(1, 3) XT_QC(1, 4)
+      XT_QC(2, 0) XT_QC(2, 1) XT_QC(2, 2) XT_QC(2, 3) XT_QC(2, 4)
+      XT_QC(3, 0) XT_QC(3, 1) XT_QC(3, 2) XT_QC(3, 3)
+      XT_QC(4, 0) XT_QC(4, 1) XT_QC(4, 2)
+      default: break;
+    }
+#undef XT_QC
+  }
   double R[ntuv(MAXL)], S[ntuv(MAXL)], M[ntuv(MAXLAB)];
   for (int q = 0; q < npp; ++q) {
     const double* pp = pair_prim + 4 * (long)(pq0 + q);
@@ -181,6 +331,18 @@ int int2e_cart(int npair, const int* pair_info, const double* pair_prim, const d
                long ldo, hipStream_t st) {
   const long n = diag ? (long)npair : (long)npair * nket;
   if (n == 0) return 0;
+  {   // the Boys table, once per device (stream-ordered before this launch)
+    static std::mutex mu;
+    static unsigned long long done = 0;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    if (dev >= 64 || !(done >> dev & 1ull)) {
+      hipLaunchKernelGGL(k_boys_init, dim3((BOYS_NT + 63) / 64), dim3(64), 0, st);
+      if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return XT_ERR_HIP;
+      if (dev < 64) done |= 1ull << dev;
+    }
+  }
   const int blk = 64;
   const dim3 grid((unsigned)((n + blk - 1) / blk));
   if (2 * lmax_orb <= 4 && 2 * lmax_orb + lket <= 8)

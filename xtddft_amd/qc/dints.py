@@ -76,23 +76,27 @@ class PairTable:
                 tabs[k] = (np.ascontiguousarray(bt.Eab[m][..., keep]), bt.p[m][keep], bt.P[m][keep])
                 self.nprim_pairs += keep.size
                 self.nprim_pairs_kept += int(keep.sum())
-        k = 0
-        for i in range(len(sh)):
-            for j in range(i + 1):
-                eab_k, p_k, P_k = tabs[k]
-                tabs[k] = None
-                k += 1
-                nca, ncb, _, npp = eab_k.shape
-                pinfo.append([sh[i].l, sh[j].l, npp, q0, e0, crow, 0, 0])
-                pprim.append(np.column_stack([p_k, P_k]))
-                eab.append(eab_k.ravel())
-                pairs.append((i, j))
-                c0s.append(crow)
-                s0s.append(srow)
-                crow += nca * ncb
-                srow += sh[i].nsph * sh[j].nsph
-                q0 += npp
-                e0 += eab_k.size
+        # pair order: by total angular momentum, then by primitive pairs (most first) -- the
+        # integral kernel runs one thread per (bra pair, ket) with the bra index fastest, so
+        # a wave's bras share their class and loop trip counts
+        tri = [(i, j) for i in range(len(sh)) for j in range(i + 1)]
+        order = sorted(range(len(tri)), key=lambda kk: (sh[tri[kk][0]].l + sh[tri[kk][1]].l,
+                                                        -tabs[kk][1].size, kk))
+        for kk in order:
+            i, j = tri[kk]
+            eab_k, p_k, P_k = tabs[kk]
+            tabs[kk] = None
+            nca, ncb, _, npp = eab_k.shape
+            pinfo.append([sh[i].l, sh[j].l, npp, q0, e0, crow, 0, 0])
+            pprim.append(np.column_stack([p_k, P_k]))
+            eab.append(eab_k.ravel())
+            pairs.append((i, j))
+            c0s.append(crow)
+            s0s.append(srow)
+            crow += nca * ncb
+            srow += sh[i].nsph * sh[j].nsph
+            q0 += npp
+            e0 += eab_k.size
         self.pinfo = np.array(pinfo, dtype=np.int32)
         self.pprim = np.concatenate(pprim) if any(x.size for x in pprim) else np.zeros((1, 4))
         self.eab = np.concatenate(eab) if any(x.size for x in eab) else np.zeros(1)
