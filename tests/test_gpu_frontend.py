@@ -133,3 +133,15 @@ def test_cholesky_mean_field_reproduces_reference(torch):
     assert abs(mf.e_tot - ref["roks_bhandhlyp_e_tot"]) < 1e-8
     e, _ = XSF_TDA(mf.to_meanfield()).kernel(nstates=10, fglobal=ref["xsf_roks_alda0_fglobal"])
     assert np.abs(np.asarray(e) - np.asarray(ref["xsf_roks_alda0_ev"])).max() / HA2EV_XSF < 1e-6
+
+
+def test_device_becke_partition_matches_host(torch):
+    """The Becke partition on the device (all atom pairs of a point block at once)
+    against the host loop over atom pairs: weights to FP64 rounding."""
+    from molecules import ch2o_mol
+    from xtddft_amd.qc.grid import gen_grids
+    for mol in (ch2o_mol(), _spdf_mol()):
+        h = gen_grids(mol)
+        d = gen_grids(mol, device=0)
+        assert np.array_equal(h.coords, d.coords)
+        assert np.abs(h.weights - d.weights).max() <= 1e-13 * np.abs(h.weights).max()

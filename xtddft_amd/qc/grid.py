@@ -148,6 +148,45 @@ def becke_partition(atom_coords, charges, coords, owner):
     return P[owner, np.arange(coords.shape[0])] / P.sum(axis=0)
 
 
+def becke_partition_device(atom_coords, charges, coords, owner, device: int = 0):
+    """becke_partition on GPU ``device`` (torch): all atom pairs of a block of points at
+    once, P_i = prod_{j != i} s(nu_ij) with the same cell function and Treutler
+    adjustment (a_ji = -a_ij and s(nu_ji) = 1 - s(nu_ij), so the ordered pairs
+    reproduce the host loop over i > j); weights equal to FP64 rounding.  The host
+    loop costs natm^2 / 2 passes over the grid (C60: 7 s)."""
+    import torch
+    natm = len(charges)
+    if natm == 1:
+        return np.ones(coords.shape[0])
+    dv = torch.device(f"cuda:{device}")
+    rad = np.sqrt(BRAGG_RADII[np.asarray(charges, dtype=np.int64)]) + 1e-200
+    rr = rad[:, None] / rad[None, :]
+    a = np.clip(0.25 * (rr.T - rr), -0.5, 0.5)
+    rij = np.linalg.norm(atom_coords[:, None, :] - atom_coords[None, :, :], axis=2)
+    np.fill_diagonal(rij, 1.0)
+    A = torch.as_tensor(a, device=dv)[:, :, None]
+    iR = torch.as_tensor(1.0 / rij, device=dv)[:, :, None]
+    X = torch.as_tensor(atom_coords, dtype=torch.float64, device=dv)
+    own = torch.as_tensor(np.asarray(owner, dtype=np.int64), device=dv)
+    ng = coords.shape[0]
+    out = torch.empty(ng, dtype=torch.float64, device=dv)
+    blk = max(1024, (1 << 26) // (natm * natm))            # ~0.5 GB per (natm, natm, blk) tensor
+    ii = torch.arange(natm, device=dv)
+    for s0 in range(0, ng, blk):
+        s1 = min(ng, s0 + blk)
+        C = torch.as_tensor(coords[s0:s1], dtype=torch.float64, device=dv)
+        d = ((X[:, None, :] - C[None, :, :]) ** 2).sum(-1).sqrt()            # (natm, m)
+        g = (d[:, None, :] - d[None, :, :]) * iR                              # nu_ij
+        g = g + A * (1 - g * g)
+        for _ in range(3):
+            g = (3 - g * g) * g * 0.5
+        sij = 0.5 - 0.5 * g
+        sij[ii, ii] = 1.0
+        P = sij.prod(dim=1)                                                   # (natm, m)
+        out[s0:s1] = P.gather(0, own[None, s0:s1])[0] / P.sum(0)
+    return out.cpu().numpy()
+
+
 @dataclass
 class Grids:
     """``mf.grids``: coords (ngrid, 3) Bohr, weights (ngrid,), per-atom radial/angular sizes."""
@@ -160,7 +199,8 @@ class Grids:
         return int(self.weights.size)
 
 
-def gen_grids(mol, level: int = 3, prune: bool = True) -> Grids:
+def gen_grids(mol, level: int = 3, prune: bool = True, device: int | None = None) -> Grids:
+    """PySCF's level-3 grid; the Becke partition on GPU ``device`` when given."""
     if level != 3:
         raise NotImplementedError("only PySCF's default grid level 3 is tabulated")
     xyz = mol.atom_coords()
@@ -175,5 +215,8 @@ def gen_grids(mol, level: int = 3, prune: bool = True) -> Grids:
     coords = np.concatenate(coords)
     weights = np.concatenate(weights)
     owner = np.concatenate(owner)
-    weights = weights * becke_partition(xyz, charges, coords, owner)
+    if device is None:
+        weights = weights * becke_partition(xyz, charges, coords, owner)
+    else:
+        weights = weights * becke_partition_device(xyz, charges, coords, owner, device)
     return Grids(coords=coords, weights=weights, atom_grid_sizes=sizes)

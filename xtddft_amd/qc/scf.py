@@ -139,7 +139,7 @@ class _SCFBase:
         if self.xctype != "HF":
             t0 = time.perf_counter()
             if self.grids is None:
-                self.grids = gen_grids(mol)
+                self.grids = gen_grids(mol, device=dev)
             self.timings["grid_s"] = time.perf_counter() - t0
             t0 = time.perf_counter()
             self.ao = mol.eval_ao(self.grids.coords, deriv=1 if self.xctype in ("GGA", "MGGA") else 0,
