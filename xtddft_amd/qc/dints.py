@@ -330,24 +330,40 @@ def eri_columns_device(mol, kets, q=None, thr: float = 0.0, device: int = 0, ome
                 qb=q, qk=qk, thr=thr)
         rows = tab.rows_to_sph(cart, device)[d["upack"]]                    # (npack, ncol) packed rows
         del cart
-        # ket side: Cartesian -> spherical per ket pair, keep the unique (mu >= nu) columns
-        cols, blocks = [], []
-        c = 0
-        for k, nc in zip(kets, nab):
+        # ket side: Cartesian -> spherical, one batched product per (l_i, l_j) class of the
+        # kets, then the unique (mu >= nu) columns times their norms -- a few uploads per
+        # batch instead of several per ket
+        cstart = np.concatenate([[0], np.cumsum(nab)[:-1]])
+        by_class = {}
+        for pos, k in enumerate(kets):
             i, j = tab.pairs[k]
-            si, sj = mol.shells[i], mol.shells[j]
-            Tk = torch.as_tensor(np.kron(_sph_transform(si.l), _sph_transform(sj.l)), device=dv)
-            mu = mol.ao_loc[i] + np.arange(si.nsph)[:, None]
-            nu = mol.ao_loc[j] + np.arange(sj.nsph)[None, :]
-            keep = (mu >= nu).ravel()
-            w = (mol._norm[mu] * mol._norm[nu]).ravel()[keep]
-            blk = torch.matmul(rows[:, c:c + nc], Tk.T)[:, torch.as_tensor(np.where(keep)[0], device=dv)]
-            blocks.append(blk * torch.as_tensor(w, device=dv)[None, :])
-            mm = np.broadcast_to(mu, (si.nsph, sj.nsph)).ravel()[keep]
-            nn = np.broadcast_to(nu, (si.nsph, sj.nsph)).ravel()[keep]
-            cols.append(mm * (mm + 1) // 2 + nn)
-            c += nc
-        return np.concatenate(cols), torch.cat(blocks, dim=1)
+            by_class.setdefault((mol.shells[i].l, mol.shells[j].l), []).append(pos)
+        tks = d.setdefault("ket_tk", {})
+        blocks, cols, sel, wts = [], [], [], []
+        off = 0
+        for (li, lj), poss in by_class.items():
+            if (li, lj) not in tks:
+                tks[(li, lj)] = torch.as_tensor(np.kron(_sph_transform(li), _sph_transform(lj)), device=dv)
+            Tk = tks[(li, lj)]
+            ns, nc = Tk.shape
+            cidx = torch.as_tensor((cstart[poss][:, None] + np.arange(nc)[None, :]).ravel(), device=dv)
+            blocks.append(torch.matmul(rows[:, cidx].reshape(-1, len(poss), nc), Tk.T).reshape(-1, len(poss) * ns))
+            for m, pos in enumerate(poss):
+                i, j = tab.pairs[kets[pos]]
+                si, sj = mol.shells[i], mol.shells[j]
+                mu = mol.ao_loc[i] + np.arange(si.nsph)[:, None]
+                nu = mol.ao_loc[j] + np.arange(sj.nsph)[None, :]
+                keep = np.where((mu >= nu).ravel())[0]
+                sel.append(off + m * ns + keep)
+                wts.append((mol._norm[mu] * mol._norm[nu]).ravel()[keep])
+                mm = np.broadcast_to(mu, (si.nsph, sj.nsph)).ravel()[keep]
+                nn = np.broadcast_to(nu, (si.nsph, sj.nsph)).ravel()[keep]
+                cols.append(mm * (mm + 1) // 2 + nn)
+            off += len(poss) * ns
+        allb = torch.cat(blocks, dim=1) if len(blocks) > 1 else blocks[0]
+        tsel = torch.as_tensor(np.concatenate(sel), device=dv)
+        tw = torch.as_tensor(np.concatenate(wts), device=dv)
+        return np.concatenate(cols), allb[:, tsel] * tw[None, :]
 
 
 # ---------------------------------------------------------------- 1-electron

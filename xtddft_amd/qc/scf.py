@@ -341,7 +341,7 @@ class ROHF(_SCFBase):
 
     def _occ(self, e, c, lab, fa):
         """ROHF occupations: core by Roothaan energy, open shells by alpha energy."""
-        ea = np.einsum('pi,pq,qi->i', c, fa, c)
+        ea = np.sum(c * (fa @ c), axis=0)              # diag(C^T F_a C) by one GEMM
         occ = np.zeros(e.size)
         counts = self._irrep_counts()
         groups = ([(np.arange(e.size), self.mol.nelec)] if counts is None else
