@@ -20,9 +20,13 @@
 // The Hermite expansion coefficients E (contraction coefficients folded in) are
 // per shell pair / ket shell and cheap: the caller prepares them.  The kernel does
 // the quartic part -- Boys functions, the Hermite integrals R_tuv by the downward
-// recursion, and the two contractions -- one thread per (bra pair, ket), the R
-// table in private memory sized by the template bucket (total order L <= 8: d
-// shells; L <= 13: f shells with auxiliary shells up to l = 7 or f f kets).
+// recursion, and the two contractions -- one thread per (bra pair, ket), the bra index
+// fastest over pairs the caller orders by class (qc/dints.py PairTable), so a wave's
+// quartets share their class.  Quartets with lab, lc <= 4 and L <= 6 (the contracted s /
+// p shells, most primitive quartets) run compile-time (t, u, v) code with the R table in
+// registers (quartet_cls); the rest keep it in private memory sized by the template
+// bucket (total order L <= 8: d shells; L <= 13: f shells with auxiliary shells up to
+// l = 7 or f f kets).
 // Schwarz screening: with bounds q_bra / q_ket, a (bra, ket) block whose bound
 // product is below q_thr is skipped (left as the caller's zeros).  Not a hot-path
 // kernel (once per mean field).  omega > 0 evaluates the long-range operator
