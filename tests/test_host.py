@@ -217,3 +217,22 @@ def test_nlc_functional_follows_the_reference():
         SF_TDA_up(mf)
     with pytest.warns(RuntimeWarning, match="NLC functional"):
         XSF_TDA(mf)
+
+
+def test_cholesky_batch_pivots_reproduce_the_block():
+    """qc/dchol.py _batch_pivots (the host half of the blocked in-batch pivoting): on a
+    rank-12 PSD block the pivots run largest-residual-first until the residual diagonal
+    is below the cut, and the factor's outer product reproduces the block; with a cut
+    above the smaller residuals it stops early and every skipped diagonal is <= cut."""
+    from xtddft_amd.qc.dchol import _batch_pivots
+    rng = np.random.default_rng(3)
+    g = rng.normal(size=(30, 12)) * 0.4 ** np.arange(12)      # decaying spectrum
+    c = g @ g.T
+    piv, lb = _batch_pivots(c, np.diag(c).copy(), 1e-10)
+    assert piv.size == 12 and piv[0] == int(np.argmax(np.diag(c)))
+    assert np.abs(lb @ lb.T - c).max() < 1e-9 * np.abs(c).max()
+    cut = 1e-3 * np.diag(c).max()
+    piv2, lb2 = _batch_pivots(c, np.diag(c).copy(), cut)
+    assert 0 < piv2.size < 12
+    assert np.array_equal(piv2, piv[:piv2.size])
+    assert (np.diag(c - lb2 @ lb2.T) <= cut * (1 + 1e-12)).all()
