@@ -18,9 +18,10 @@
 //   * the rows4 reduction of a pair's per-lane partials runs once per (pair, chunk); the
 //     chunks of one pair are summed in the output (the same lane reads back what it wrote
 //     a chunk earlier; the old value is prefetched when the pair starts).
+//   * the next chunk's weight lines are pulled into L2 during the wave's last pair of a chunk;
 //   * the blocks of the last, partial round over the CUs split their trial pairs S ways
 //     (pair subsets p = s (mod S)): that round then takes a fraction of a block time
-//     instead of a whole one (n = 200 000, 3125 = 12 x 256 + 53 blocks: 0.851 -> 0.821 ms
+//     instead of a whole one (n = 200 000, 3125 = 12 x 256 + 53 blocks: 0.814 -> 0.800 ms
 //     at S = 4, tools/xcws_probe.hip).
 // Operand conventions are those of xc_rho_w (xt_internal.h): Zp readable 7 rows past O
 // and 31 columns past V (zeroed slack), PhiO / dPhiV rows past n are not read.
