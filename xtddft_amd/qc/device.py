@@ -86,7 +86,9 @@ class DeviceEngine:
         return c
 
     # ------------------------------------------------------------ J / K
-    def get_jk(self, dms, with_j=True, with_k=True):
+    def get_jk(self, dms, with_j=True, with_k=True, factors=None):
+        """J / K of densities dms; ``factors`` (C_s with dms[s] = C_s C_s^T, from the SCF's
+        orbitals) lets K skip the eigendecomposition of each density."""
         torch = self.torch
         d = np.asarray(dms, dtype=np.float64)
         shape = d.shape
@@ -98,16 +100,34 @@ class DeviceEngine:
             gam = self._mm(b2, dt.reshape(-1, n * n), tb=1)                  # (P, nset)
             vj = self._mm(gam, b2, ta=1).reshape(shape).cpu().numpy()        # (nset, n^2)
         if with_k:
-            vk = np.stack([self._k(d.reshape(-1, n, n)[x], dt[x]) for x in range(dt.shape[0])]).reshape(shape)
+            if factors is not None and len(factors) == dt.shape[0]:
+                vk = np.stack([self._k_factor(np.asarray(f, dtype=np.float64)) for f in factors]).reshape(shape)
+            else:
+                vk = np.stack([self._k(d.reshape(-1, n, n)[x], dt[x]) for x in range(dt.shape[0])]).reshape(shape)
         return vj, vk
 
-    def get_k(self, dms, lr=False):
-        """K[D] (lr: the long-range K_LR[D]) for each density of dms."""
+    def _k_factor(self, c, B=None):
+        """K[C C^T] = sum_P (B_P C)(B_P C)^T."""
+        torch = self.torch
+        B = self.B if B is None else B
+        n, P = self.n, B.shape[0]
+        r = c.shape[1]
+        if r == 0:
+            return np.zeros((n, n))
+        vt = torch.as_tensor(np.ascontiguousarray(c), device=self.dev)
+        t = self._mm(B.reshape(P * n, n), vt).reshape(P, n, r)             # T_P = B_P C
+        return self._reduce_p(t, t, nt=True).cpu().numpy()                 # sum_P T_P T_P^T
+
+    def get_k(self, dms, lr=False, factors=None):
+        """K[D] (lr: the long-range K_LR[D]) for each density of dms (``factors`` as in
+        get_jk)."""
         d = np.asarray(dms, dtype=np.float64)
-        dt = self.torch.as_tensor(np.ascontiguousarray(d.reshape(-1, self.n, self.n)), device=self.dev)
         B = self.B_lr if lr else self.B
         if B is None:
             raise ValueError("no long-range factor: the functional is not range-separated")
+        if factors is not None and len(factors) == d.reshape(-1, self.n, self.n).shape[0]:
+            return np.stack([self._k_factor(np.asarray(f, dtype=np.float64), B) for f in factors]).reshape(d.shape)
+        dt = self.torch.as_tensor(np.ascontiguousarray(d.reshape(-1, self.n, self.n)), device=self.dev)
         return np.stack([self._k(d.reshape(-1, self.n, self.n)[x], dt[x], B) for x in range(dt.shape[0])]
                         ).reshape(d.shape)
 

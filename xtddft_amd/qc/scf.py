@@ -170,10 +170,20 @@ class _SCFBase:
         return self.mol.energy_nuc()
 
     # -------------------------------------------------------- potentials
+    def _factored(self, dms, factors):
+        """dms built as C_s C_s^T from orbitals: remember the factors for the device
+        exchange (K[D] = sum_P (B_P C)(B_P C)^T, no eigendecomposition of D)."""
+        self._dm_factors = (dms, factors)
+        return dms
+
+    def _factors_of(self, dm):
+        f = getattr(self, "_dm_factors", None)
+        return f[1] if f is not None and f[0] is dm else None
+
     def get_jk(self, mol=None, dm=None, hermi=1, with_j=True, with_k=True):
         """PySCF incore convention: vj = (ij|kl) D_kl, vk = (ij|kl) D_jk -> [i,l]."""
         if self.device_engine is not None:
-            return self.device_engine.get_jk(dm, with_j, with_k)
+            return self.device_engine.get_jk(dm, with_j, with_k, factors=self._factors_of(dm))
         if self.with_df is not None:
             return self.with_df.get_jk(dm, with_j, with_k)
         d = np.asarray(dm, dtype=np.float64)
@@ -195,7 +205,7 @@ class _SCFBase:
         if self.omega == 0:
             raise ValueError(f"{self.xc} is not range-separated")
         if self.device_engine is not None:
-            return self.device_engine.get_k(dm, lr=True)
+            return self.device_engine.get_k(dm, lr=True, factors=self._factors_of(dm))
         if self.with_df is not None:
             return self.with_df.get_k_lr(dm, self.omega)
         d = np.asarray(dm, dtype=np.float64)
@@ -354,11 +364,10 @@ class ROHF(_SCFBase):
             occ[opn] = 1
         return occ
 
-    @staticmethod
-    def _dms(c, occ):
+    def _dms(self, c, occ):
         ca = c[:, occ >= 1]
         cb = c[:, occ >= 2]
-        return np.asarray([ca @ ca.T, cb @ cb.T])
+        return self._factored(np.asarray([ca @ ca.T, cb @ cb.T]), [ca, cb])
 
     def _grad(self, c, occ, fa, fb):
         fam = c.T @ fa @ c
@@ -451,6 +460,10 @@ class UHF(_SCFBase):
                     occ[s][idx[np.argsort(es[s][idx], kind="stable")[:nab[s]]]] = 1
         return occ
 
+    def _uhf_dms(self, cs, occ):
+        f = [cs[t][:, occ[t] > 0] for t in range(2)]
+        return self._factored(np.asarray([f[t] @ f[t].T for t in range(2)]), f)
+
     def kernel(self, dm0=None):
         self.build()
         s = self.s1e
@@ -461,8 +474,7 @@ class UHF(_SCFBase):
             cs = (c, c)
         else:
             cs = None
-        dms = (np.asarray([cs[t][:, occ[t] > 0] @ cs[t][:, occ[t] > 0].T for t in range(2)])
-               if dm0 is None else np.asarray(dm0))
+        dms = (self._uhf_dms(cs, occ) if dm0 is None else np.asarray(dm0))
         diis_f, diis_e = [], []
         e_last = None
         for cycle in range(self.max_cycle):
@@ -485,7 +497,7 @@ class UHF(_SCFBase):
                     o = occ[t] > 0
                     g += np.sum(fm[np.ix_(~o, o)] ** 2)
                 gnorm = np.sqrt(g)
-            dms_new = np.asarray([res[t][1][:, occ[t] > 0] @ res[t][1][:, occ[t] > 0].T for t in range(2)])
+            dms_new = self._uhf_dms([res[0][1], res[1][1]], occ)
             if self.verbose:
                 print(f"cycle {cycle} E= {e_tot:.12f} |g|= {gnorm:.2e}")
             if e_last is not None and abs(e_tot - e_last) < self.conv_tol and gnorm < tol_grad:
