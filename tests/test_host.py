@@ -236,3 +236,20 @@ def test_cholesky_batch_pivots_reproduce_the_block():
     assert 0 < piv2.size < 12
     assert np.array_equal(piv2, piv[:piv2.size])
     assert (np.diag(c - lb2 @ lb2.T) <= cut * (1 + 1e-12)).all()
+
+
+def test_scf_density_factors_follow_the_array():
+    """qc/scf.py: the orbital factors handed to the device exchange belong to the exact
+    density array they were built with, and are dropped once it is changed in place."""
+    from xtddft_amd.qc import ROKS
+    from molecules import hf_mol
+    mf = ROKS(hf_mol(), "HF")
+    c = np.linalg.qr(np.random.default_rng(0).normal(size=(mf.mol.nao, mf.mol.nao)))[0]
+    occ = np.zeros(mf.mol.nao)
+    occ[:4], occ[4] = 2, 1
+    dms = mf._dms(c, occ)
+    f = mf._factors_of(dms)
+    assert f is not None and np.allclose(f[0] @ f[0].T, dms[0]) and np.allclose(f[1] @ f[1].T, dms[1])
+    assert mf._factors_of(dms.copy()) is None
+    dms *= 0.5
+    assert mf._factors_of(dms) is None

@@ -173,12 +173,13 @@ class _SCFBase:
     def _factored(self, dms, factors):
         """dms built as C_s C_s^T from orbitals: remember the factors for the device
         exchange (K[D] = sum_P (B_P C)(B_P C)^T, no eigendecomposition of D)."""
-        self._dm_factors = (dms, factors)
+        self._dm_factors = (dms, factors, float(np.sum(dms)))
         return dms
 
     def _factors_of(self, dm):
+        """The factors of exactly that density array, unless it was changed in place since."""
         f = getattr(self, "_dm_factors", None)
-        return f[1] if f is not None and f[0] is dm else None
+        return f[1] if f is not None and f[0] is dm and float(np.sum(dm)) == f[2] else None
 
     def get_jk(self, mol=None, dm=None, hermi=1, with_j=True, with_k=True):
         """PySCF incore convention: vj = (ij|kl) D_kl, vk = (ij|kl) D_jk -> [i,l]."""
